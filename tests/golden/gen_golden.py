@@ -1,0 +1,356 @@
+"""Generate the golden fixtures under tests/golden/ from the reference itself.
+
+Runs ONLY in the build container (the reference is not present on the GPU box).
+It imports A-Andrews/Muzero-Hanoi from /root/reference with a one-line `seaborn` stub
+(seaborn is imported at module top by reference utils.py:5 but only used for plotting),
+never writes into the reference tree (PYTHONDONTWRITEBYTECODE), and saves small .npz/.json
+files of INPUTS and OUTPUTS only -- no reference source travels with them.
+
+    python tests/golden/gen_golden.py            # regenerate every fixture
+
+Fixtures (see tests/golden/README.md):
+  env_N{3,4,7}.npz        every state x action through TowersOfHanoi.step (env/hanoi.py:47-84)
+  env_maxsteps.npz        step-counter / goal quirk sequences (env/hanoi.py:65-80)
+  solver_N{3,4,7}.npz     hanoi_solver for all 3^N states (env/hanoi_utils.py:4-26)
+  weights_N{N}_s{seed}.npz  MuZeroNet(TD_return=...) state_dict after torch.manual_seed(seed)
+  mlp_N{N}_s{seed}.npz    initial/recurrent inference I/O + raw logits (networks.py:71-150)
+  replay_<case>.npz       full run_mcts traces: every network call's inputs/outputs, RNG events,
+                          final visits / pi / rootQ / action / min-max (MCTS/mcts.py:34-126)
+"""
+import json
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+sys.modules.setdefault("seaborn", types.ModuleType("seaborn"))
+sys.path.insert(0, REF)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from env.hanoi import TowersOfHanoi  # noqa: E402
+from env.hanoi_utils import hanoi_solver  # noqa: E402
+from MCTS.mcts import MCTS  # noqa: E402
+from networks import MuZeroNet  # noqa: E402
+
+torch.set_num_threads(1)
+
+WEIGHT_KEYS = [
+    f"{net}.{layer}.{kind}"
+    for net in ("representation_net", "dynamic_net", "rwd_net", "policy_net", "value_net")
+    for layer in (0, 2)
+    for kind in ("weight", "bias")
+]
+
+
+def state_index(state, n):
+    idx = 0
+    for s in state:
+        idx = idx * 3 + int(s)
+    return idx
+
+
+# --------------------------------------------------------------------------- env
+def gen_env(n):
+    env = TowersOfHanoi(N=n, max_steps=10**9)
+    ns = len(env.states)
+    nxt = np.zeros((ns, 6), np.int32)  # env.c_state index after the step
+    moved = np.zeros((ns, 6), np.int32)  # state encoded in the returned one-hot
+    rwd = np.zeros((ns, 6), np.float64)
+    done = np.zeros((ns, 6), np.uint8)
+    illegal = np.zeros((ns, 6), np.uint8)
+    legal = np.zeros((ns, 6), np.uint8)
+    for i, st in enumerate(env.states):
+        for a in range(6):
+            env.reset()
+            env.c_state = st
+            env.step_counter = 0
+            legal[i, a] = env._move_allowed(env.moves[a])
+            obs, r, d, ill = env.step(a)
+            onehot = obs.reshape(n, 3)
+            assert onehot.sum() == n
+            moved[i, a] = state_index(onehot.argmax(1), n)
+            nxt[i, a] = state_index(env.c_state, n)
+            rwd[i, a] = r
+            done[i, a] = d
+            illegal[i, a] = ill
+    np.savez_compressed(
+        os.path.join(HERE, f"env_N{n}.npz"),
+        n=n, next_state=nxt, moved_state=moved, reward=rwd, done=done, illegal=illegal,
+        legal=legal, goal=state_index(env.goal, n), n_states=ns,
+        moves=np.array(env.moves, np.int32),
+    )
+
+
+def gen_env_maxsteps():
+    """Sequences exercising step_counter / max_steps / goal-reset (env/hanoi.py:65-80)."""
+    rows = []
+    rng = np.random.RandomState(7)
+    for n, max_steps, init_idx in [(3, 5, 0), (3, 200, 0), (4, 7, 5), (3, 3, 25)]:
+        env = TowersOfHanoi(N=n, max_steps=max_steps, init_state_idx=init_idx)
+        env.reset()
+        for t in range(3 * max_steps if max_steps < 50 else 60):
+            if not env.reset_check:
+                env.reset()
+            a = int(rng.randint(6))
+            before = state_index(env.c_state, n)
+            ctr_before = env.step_counter
+            obs, r, d, ill = env.step(a)
+            rows.append((n, max_steps, init_idx, before, ctr_before, a,
+                         state_index(obs.reshape(n, 3).argmax(1), n),
+                         state_index(env.c_state, n), float(r), int(d), int(ill),
+                         env.step_counter, int(env.reset_check)))
+    # an optimal solve that reaches the goal: c_state must NOT advance on the goal step
+    env = TowersOfHanoi(N=3, max_steps=200, init_state_idx=state_index((1, 2, 2), 3))
+    env.reset()
+    before = state_index(env.c_state, 3)
+    a = env.moves.index((1, 2))
+    obs, r, d, ill = env.step(a)
+    rows.append((3, 200, env.init_state_idx, before, 0, a,
+                 state_index(obs.reshape(3, 3).argmax(1), 3), state_index(env.c_state, 3),
+                 float(r), int(d), int(ill), env.step_counter, int(env.reset_check)))
+    arr = np.array(rows, dtype=np.float64)
+    np.savez_compressed(
+        os.path.join(HERE, "env_maxsteps.npz"), rows=arr,
+        columns=np.array(["n", "max_steps", "init_idx", "state_before", "ctr_before", "action",
+                          "moved_state", "c_state_after", "reward", "done", "illegal",
+                          "ctr_after", "reset_check_after"]),
+    )
+
+
+def gen_solver(n):
+    env = TowersOfHanoi(N=n, max_steps=1)
+    vals = np.array([hanoi_solver(tuple(s)) for s in env.states], np.int32)
+    vals_g0 = np.array([hanoi_solver(tuple(s), 0) for s in env.states], np.int32)
+    np.savez_compressed(os.path.join(HERE, f"solver_N{n}.npz"), n=n, moves=vals, moves_goal0=vals_g0)
+
+
+# --------------------------------------------------------------------------- network
+def make_net(n, seed, td=True):
+    torch.manual_seed(seed)
+    return MuZeroNet(rpr_input_s=3 * n, action_s=6, lr=0.002, device="cpu", TD_return=td)
+
+
+def save_weights(net, n, seed, td=True):
+    sd = net.state_dict()
+    path = os.path.join(HERE, f"weights_N{n}_s{seed}{'' if td else '_mc'}.npz")
+    np.savez_compressed(path, **{k: sd[k].numpy() for k in WEIGHT_KEYS})
+
+
+def gen_mlp(n, seed, td=True, batch=24):
+    net = make_net(n, seed, td)
+    save_weights(net, n, seed, td)
+    rng = np.random.RandomState(1000 + seed + n)
+    # observations: one-hot Hanoi states + a few arbitrary float vectors (noise-injection style)
+    states = rng.randint(0, 3, size=(batch, n))
+    x = np.zeros((batch, 3 * n), np.float32)
+    for b in range(batch):
+        x[b, np.arange(n) * 3 + states[b]] = 1.0
+    x[-4:] = rng.uniform(-1, 1, size=(4, 3 * n)).astype(np.float32)
+    h_in = rng.uniform(0, 1, size=(batch, 64)).astype(np.float32)
+    a_in = rng.randint(0, 6, size=batch).astype(np.int64)
+
+    ii_h, ii_r, ii_pi, ii_v = [], [], [], []
+    ri_h, ri_r, ri_pi, ri_v = [], [], [], []
+    pol_logits0, val_logits0 = [], []
+    pol_logits1, val_logits1, rwd_logits1, hraw1 = [], [], [], []
+    with torch.no_grad():
+        for b in range(batch):
+            xt = torch.from_numpy(x[b])
+            h, r, pi, v = net.initial_inference(xt)
+            ii_h.append(h); ii_r.append(r); ii_pi.append(pi); ii_v.append(v)
+            hs = net.represent(xt)
+            pol_logits0.append(net.policy_net(hs).numpy())
+            val_logits0.append(net.value_net(hs).numpy())
+
+            ht = torch.from_numpy(h_in[b])
+            at = torch.nn.functional.one_hot(torch.tensor([a_in[b]]), 6).squeeze().float()
+            h2, r2, pi2, v2 = net.recurrent_inference(ht, at)
+            ri_h.append(h2); ri_r.append(r2); ri_pi.append(pi2); ri_v.append(v2)
+            hr = net.dynamic_net(torch.cat([ht, at], -1))
+            hraw1.append(hr.numpy())
+            rwd_logits1.append(net.rwd_net(hr).numpy())
+            hn = net.normalize_h_state(hr)
+            pol_logits1.append(net.policy_net(hn).numpy())
+            val_logits1.append(net.value_net(hn).numpy())
+    np.savez_compressed(
+        os.path.join(HERE, f"mlp_N{n}_s{seed}{'' if td else '_mc'}.npz"),
+        n=n, seed=seed, td=int(td), x=x, h_in=h_in, a_in=a_in,
+        ii_h=np.array(ii_h, np.float32), ii_rwd=np.array(ii_r, np.float64),
+        ii_pi=np.array(ii_pi, np.float32), ii_value=np.array(ii_v, np.float64),
+        ii_policy_logits=np.array(pol_logits0, np.float32),
+        ii_value_logits=np.array(val_logits0, np.float32),
+        ri_h=np.array(ri_h, np.float32), ri_rwd=np.array(ri_r, np.float64),
+        ri_pi=np.array(ri_pi, np.float32), ri_value=np.array(ri_v, np.float64),
+        ri_h_raw=np.array(hraw1, np.float32), ri_rwd_logits=np.array(rwd_logits1, np.float32),
+        ri_policy_logits=np.array(pol_logits1, np.float32),
+        ri_value_logits=np.array(val_logits1, np.float32),
+    )
+
+
+# --------------------------------------------------------------------------- search traces
+class Recorder:
+    """Duck-typed network (MCTS/mcts.py:50,96,102): calls the real MuZeroNet, records I/O."""
+
+    def __init__(self, net):
+        self.net = net
+        self.num_actions = net.num_actions
+        self.calls = []
+
+    def initial_inference(self, x):
+        out = self.net.initial_inference(x)
+        self.calls.append(("i", x.numpy().copy(), -1, out))
+        return out
+
+    def recurrent_inference(self, h, a):
+        out = self.net.recurrent_inference(h, a)
+        self.calls.append(("r", h.numpy().copy(), int(a.argmax()), out))
+        return out
+
+
+class TracingMCTS(MCTS):
+    """Subclass (in this script only) that captures the root visit histogram and the
+    Dirichlet-mixed priors; the reference files are not modified."""
+
+    def generate_play_policy(self, visits_count, temperature):
+        self.last_visits = np.asarray(visits_count).copy()
+        return super().generate_play_policy(visits_count, temperature)
+
+    def add_dirichlet_noise(self, prob, eps=0.25, alpha=0.25):
+        out = super().add_dirichlet_noise(prob, eps=eps, alpha=alpha)
+        self.last_noised = np.asarray(out, np.float64).copy()
+        return out
+
+
+def gen_replay(name, n, s, n_roots, deterministic, alpha, temperature, seed=1, wseed=0,
+               shared=False, td=True, discount=0.8):
+    net = make_net(n, wseed, td)
+    np.random.seed(seed)
+    rec_choice = []
+    orig_choice = np.random.choice
+
+    def choice(a, *args, **kw):
+        r = orig_choice(a, *args, **kw)
+        size = a if isinstance(a, (int, np.integer)) else len(a)
+        rec_choice.append((len(rec_per_root) - 1, size, "p" in kw, int(r)))
+        return r
+
+    np.random.choice = choice
+    env = TowersOfHanoi(N=n, max_steps=200)
+    goal = state_index(env.goal, n)
+    rs = np.random.RandomState(seed + 17)  # root states (separate stream: not the global RNG)
+    root_idx = []
+    while len(root_idx) < n_roots:
+        i = int(rs.randint(3 ** n))
+        if i != goal:
+            root_idx.append(i)
+    rec_per_root = []
+    out = dict(visits=[], pi=[], rootQ=[], action=[], mm_max=[], mm_min=[], noised=[],
+               latent=[], calls_h=[], calls_a=[], out_h=[], out_rwd=[], out_pi=[], out_v=[],
+               obs=[])
+    mcts = None
+    try:
+        for r, idx in enumerate(root_idx):
+            rec_per_root.append(r)
+            if mcts is None or not shared:
+                mcts = TracingMCTS(discount=discount, root_dirichlet_alpha=alpha,
+                                   n_simulations=s, batch_s=256, device="cpu")
+            mcts.last_noised = None
+            st = env.states[idx]
+            obs = np.zeros(3 * n)
+            obs[np.arange(n) * 3 + np.array(st)] = 1.0
+            recorder = Recorder(net)
+            action, pi, q = mcts.run_mcts(obs, recorder, temperature, deterministic)
+            out["visits"].append(mcts.last_visits.astype(np.int32))
+            out["pi"].append(np.asarray(pi, np.float64))
+            out["rootQ"].append(float(q))
+            out["action"].append(int(action))
+            out["mm_max"].append(float(mcts.min_max_stats.maximum))
+            out["mm_min"].append(float(mcts.min_max_stats.minimum))
+            out["noised"].append(mcts.last_noised if mcts.last_noised is not None
+                                 else np.full(6, np.nan))
+            lat = [int(t.item()) for t in mcts.return_latent_actions()]
+            out["latent"].append(lat + [-1] * (s + 2 - len(lat)))
+            out["obs"].append(obs)
+            calls = recorder.calls
+            assert calls[0][0] == "i" and len(calls) == s + 1
+            out["calls_h"].append(np.array([c[1] if c[0] == "r" else np.zeros(64, np.float32)
+                                            for c in calls], np.float32))
+            out["calls_a"].append(np.array([c[2] for c in calls], np.int32))
+            out["out_h"].append(np.array([c[3][0] for c in calls], np.float32))
+            out["out_rwd"].append(np.array([c[3][1] for c in calls], np.float64))
+            out["out_pi"].append(np.array([c[3][2] for c in calls], np.float32))
+            out["out_v"].append(np.array([c[3][3] for c in calls], np.float64))
+    finally:
+        np.random.choice = orig_choice
+    ch = np.array(rec_choice, np.int64).reshape(-1, 4)
+    np.savez_compressed(
+        os.path.join(HERE, f"replay_{name}.npz"),
+        n=n, s=s, seed=seed, wseed=wseed, td=int(td), deterministic=int(deterministic),
+        alpha=alpha, temperature=temperature, shared=int(shared), discount=discount,
+        root_idx=np.array(root_idx, np.int32), obs=np.array(out["obs"], np.float64),
+        visits=np.array(out["visits"]), pi=np.array(out["pi"]),
+        rootQ=np.array(out["rootQ"]), action=np.array(out["action"], np.int32),
+        mm_max=np.array(out["mm_max"]), mm_min=np.array(out["mm_min"]),
+        noised=np.array(out["noised"], np.float64), latent=np.array(out["latent"], np.int32),
+        calls_h=np.array(out["calls_h"]), calls_a=np.array(out["calls_a"]),
+        out_h=np.array(out["out_h"]), out_rwd=np.array(out["out_rwd"]),
+        out_pi=np.array(out["out_pi"]), out_v=np.array(out["out_v"]),
+        choice_events=ch,  # (root, n_candidates, has_p, result)
+    )
+    return ch
+
+
+REPLAY_CASES = [
+    # name, n, s, roots, deterministic, alpha, T, extra
+    ("n3s25_det", 3, 25, 8, True, 0.0, 1.0, {}),
+    ("n3s25_sto", 3, 25, 8, False, 0.25, 1.0, {}),
+    ("n4s50_sto", 4, 50, 8, False, 0.25, 1.0, {}),
+    ("n4s50_det_t0", 4, 50, 6, True, 0.25, 0.0, {}),
+    ("n4s50_sto_t05", 4, 50, 6, False, 0.25, 0.5, {}),
+    ("n4s50_sto_t01", 4, 50, 4, False, 0.25, 0.1, {}),
+    ("n4s50_alpha03", 4, 50, 4, False, 0.3, 1.0, {}),
+    ("n4s50_shared", 4, 50, 6, False, 0.25, 1.0, {"shared": True}),
+    ("n4s200_sto", 4, 200, 3, False, 0.25, 1.0, {}),
+    ("n7s100_sto", 7, 100, 3, False, 0.25, 1.0, {}),
+    ("n3s25_mc", 3, 25, 4, False, 0.25, 1.0, {"td": False}),
+    ("n4s1_sto", 4, 1, 4, False, 0.25, 1.0, {}),
+]
+
+
+def main():
+    for n in (3, 4, 7):
+        gen_env(n)
+        gen_solver(n)
+    gen_env_maxsteps()
+    for n in (3, 4, 7):
+        gen_mlp(n, 0)
+    gen_mlp(3, 0, td=False)
+    gen_mlp(4, 1)
+    summary = {}
+    for name, n, s, roots, det, alpha, t, extra in REPLAY_CASES:
+        ch = gen_replay(name, n, s, roots, det, alpha, t, **extra)
+        ties = ch[(ch[:, 2] == 0) & (ch[:, 1] > 1)]
+        summary[name] = {"choice_calls": int(len(ch)), "multi_candidate_ties": int(len(ties)),
+                         "tie_sizes": sorted(set(int(v) for v in ties[:, 1]))}
+    with open(os.path.join(HERE, "rng_order.json"), "w") as f:
+        json.dump({
+            "order_per_run_mcts": [
+                "np.random.dirichlet(np.ones(6,float32)*alpha) if not deterministic and alpha>0 and eps>0 (MCTS/mcts.py:57-66,149)",
+                "np.random.choice(argmax-set) at EVERY best_child (MCTS/node.py:86); a 1-element set draws nothing",
+                "np.random.choice(6, p=pi) -> one random_sample() double if not deterministic (MCTS/mcts.py:118-120)",
+            ],
+            "observed": summary,
+            "numpy": np.__version__, "torch": torch.__version__,
+        }, f, indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()
