@@ -1,0 +1,162 @@
+/*
+ * mzh.h -- C ABI of libmzh.so: MI355X-native (gfx950 HIP) batched MuZero-MCTS + Tower-of-Hanoi.
+ *
+ * The reference (A-Andrews/Muzero-Hanoi) is pure Python; its "plugin boundary" is the duck-typed
+ * Python API that training_main.py / Muzero.py / the acting scripts call.  Each entry point below
+ * replaces one of those interfaces (cited file:line); the Python host layer in muzero-hanoi_amd/
+ * binds them with ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - Every buffer argument is a DEVICE pointer owned by the caller (e.g. a torch tensor's
+ *    data_ptr()), except where "host" is written.  Shapes are row-major; B = batch of roots/envs.
+ *  - Calls are asynchronous and stream-ordered on `stream` (a hipStream_t; NULL = null stream).
+ *  - Every function returns an int status (MZH_OK = 0, negative on error) and never throws;
+ *    mzh_last_error() returns a thread-local message for the last failure.
+ *  - An engine is bound to one device and is not re-entrant across threads (one engine per
+ *    device/stream, like the reference's single MCTS instance, MCTS/mcts.py:23).
+ *  - No CPU fallback exists: without a HIP device every compute call fails with MZH_ERR_HIP.
+ */
+#ifndef MZH_ABI_H_
+#define MZH_ABI_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MZH_ABI_VERSION 1
+
+#define MZH_OK 0
+#define MZH_ERR_ARG (-1)         /* bad argument / shape (ValueError in Python)              */
+#define MZH_ERR_HIP (-2)         /* HIP runtime error / no device (RuntimeError)              */
+#define MZH_ERR_CAPACITY (-3)    /* B > max_roots or n_sims > max_sims of the engine          */
+#define MZH_ERR_STATE (-4)       /* weights not loaded                                        */
+#define MZH_ERR_TEMPERATURE (-5) /* temperature outside [0,1] (mcts.py:163-166 ValueError)    */
+
+#define MZH_ACTIONS 6   /* itertools.permutations(range(3), 2), env/hanoi.py:39-41 */
+#define MZH_LATENT 64   /* reprs_output_size, networks.py:22 */
+#define MZH_HIDDEN 256  /* h1_s, networks.py:21 */
+
+/* search flags */
+#define MZH_FLAG_NP1_UCB 1u /* UCB rounding of NumPy 1.x (the reference's pin, requirements.txt:17):
+                               U = fl32(fl64(prior * w)); default is NumPy 2: fl32(prior * fl32(w)) */
+
+typedef struct mzh_engine mzh_engine;
+typedef void* mzh_stream; /* hipStream_t */
+
+int mzh_abi_version(void);
+const char* mzh_last_error(void);
+int mzh_device_count(int* count);
+
+/* ---------------------------------------------------------------------------------------------
+ * Engine.  Replaces the state the reference keeps in Python objects: the MuZeroNet weights
+ * (networks.py:39-67) and the per-search node pool of MCTS/node.py (flat SoA tree workspace).
+ *   n_disks   : Hanoi N (observation = 3N one-hot, env/hanoi.py:26-28, utils.py:9-25)
+ *   max_sims  : largest n_simulations a search on this engine may use (mcts.py:30)
+ *   max_roots : largest root batch B
+ *   support   : 33 (TD_return=True) or 1 (TD_return=False), networks.py:34-37
+ * ------------------------------------------------------------------------------------------- */
+int mzh_create(int device, int n_disks, int max_sims, int max_roots, int support, mzh_engine** out);
+int mzh_destroy(mzh_engine* eng);
+
+/* Number of floats of the canonical flat weight vector: the 20 tensors of MuZeroNet.state_dict()
+ * (networks.py:39-67) concatenated in the order
+ *   {representation,dynamic,rwd,policy,value}_net.{0,2}.{weight,bias},
+ * each in torch layout (nn.Linear weight [out][in] row-major). */
+int mzh_weights_size(int n_disks, int support, size_t* n_floats);
+
+/* Upload + repack (host pointer, canonical layout) into the MFMA fragment layout on the device.
+ * Replaces reading MuZeroNet parameters at inference time (networks.py:71-150). Synchronous. */
+int mzh_load_weights(mzh_engine* eng, const float* flat_host, size_t n_floats);
+
+/* ---------------------------------------------------------------------------------------------
+ * Environment: TowersOfHanoi (env/hanoi.py), batched over B independent envs.
+ * state[B][n] uint8 peg of disc d (disc 0 = smallest), the reference's tuple c_state layout.
+ * ------------------------------------------------------------------------------------------- */
+
+/* TowersOfHanoi.step (env/hanoi.py:47-84) for every env b:
+ *   state      in/out  c_state (unchanged on illegal moves and on the goal step, hanoi.py:65-74)
+ *   action     in      index into moves = [(0,1),(0,2),(1,0),(1,2),(2,0),(2,1)]
+ *   moved      out     state encoded by the returned observation (nullable)
+ *   obs        out     oneHot_encoding(moved) as float32 [B][3n] (nullable; utils.py:9-25)
+ *   reward     out     int8 code: 0 -> 0, 1 -> 100 (goal), -1 -> -100/1000 (illegal)
+ *   done, illegal out  uint8
+ *   step_ctr   in/out  step_counter (hanoi.py:50-80; illegal steps count, reset on done)
+ *   active     in/out  reset_check (hanoi.py:49); stepping an inactive env is the reference's
+ *                      AssertionError: the env is left untouched, reward = -2 and *err_count += 1
+ *   err_count  out     nullable device int32 accumulator */
+int mzh_env_step(int n_disks, int goal_peg, int max_steps, int B, uint8_t* state,
+                 const int32_t* action, uint8_t* moved, float* obs, int8_t* reward, uint8_t* done,
+                 uint8_t* illegal, int32_t* step_ctr, uint8_t* active, int32_t* err_count,
+                 mzh_stream stream);
+
+/* _move_allowed for all 6 moves (env/hanoi.py:117-139): bit a of mask[b] = move a legal. */
+int mzh_legal_mask(int n_disks, int B, const uint8_t* state, uint8_t* mask, mzh_stream stream);
+
+/* oneHot_encoding (utils.py:9-25): obs[b][3d + state[b][d]] = 1, float32. */
+int mzh_encode_obs(int n_disks, int B, const uint8_t* state, float* obs, mzh_stream stream);
+
+/* hanoi_solver (env/hanoi_utils.py:4-26): minimal moves to put every disc on goal_peg. */
+int mzh_hanoi_solver(int n_disks, int goal_peg, int B, const uint8_t* state, int32_t* moves,
+                     mzh_stream stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Network inference (MuZeroNet.initial_inference / recurrent_inference, networks.py:71-116),
+ * batched over B rows.  Output pointers other than h may be NULL.
+ *   h [B][64] normalised latent; reward [B] (0 for initial); pi [B][6] softmax policy;
+ *   value [B] transformed value; *_logits raw head outputs ([B][6], [B][support]).
+ * ------------------------------------------------------------------------------------------- */
+int mzh_initial_inference(mzh_engine* eng, int B, const float* obs, float* h, float* reward,
+                          float* pi, float* value, float* policy_logits, float* value_logits,
+                          mzh_stream stream);
+int mzh_recurrent_inference(mzh_engine* eng, int B, const float* h_in, const int32_t* action,
+                            float* h, float* reward, float* pi, float* value,
+                            float* policy_logits, float* value_logits, float* reward_logits,
+                            mzh_stream stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Batched search: B independent MCTS.run_mcts calls (MCTS/mcts.py:34-126), one per root, all
+ * simulations (select -> expand via the MLP -> backup) inside one fused kernel launch.
+ * Each root carries its own MinMaxStats (utils_mcts.py): fresh unless minmax_in is given.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct mzh_search_args {
+  int32_t B;             /* roots */
+  int32_t n_sims;        /* n_simulations (mcts.py:30) */
+  double discount;       /* mcts.py:27 */
+  double eps;            /* root_exploration_eps (mcts.py:20) */
+  double temperature;    /* generate_play_policy temperature (mcts.py:154-176) */
+  int32_t deterministic; /* argmax action instead of sampling (mcts.py:115-120) */
+  uint32_t flags;        /* MZH_FLAG_* */
+  /* inputs */
+  const float* obs;         /* [B][3n] root observations (MLP mode) */
+  const double* noise;      /* [B][6] Dirichlet draws, NULL = no noise (mcts.py:57-66) */
+  const int32_t* tie_idx;   /* [B] pre-drawn index of np.random.choice for the first 6-way tie */
+  const double* action_u;   /* [B] pre-drawn random_sample() for choice(6, p=pi); NULL if det. */
+  const double* minmax_in;  /* [B][2] (maximum, minimum) or NULL (fresh: -inf, +inf) */
+  /* replay (tree-only) inputs: network outputs recorded per simulation, used instead of the MLP
+   * by mzh_search_replay */
+  const float* rp_root_pi; /* [B][6] */
+  const float* rp_pi;      /* [B][n_sims][6] */
+  const float* rp_reward;  /* [B][n_sims] */
+  const float* rp_value;   /* [B][n_sims] */
+  /* outputs (visits required, others nullable) */
+  int32_t* visits;      /* [B][6] root child_N (node.py:133-136) */
+  double* root_q;       /* [B] root_node.Q (node.py:125-131) */
+  double* minmax_out;   /* [B][2] */
+  int32_t* extra_ties;  /* [B] argmax ties beyond the first (RNG stream divergence indicator) */
+  int32_t* action;      /* [B] chosen action (mcts.py:115-122) */
+  double* pi;           /* [B][6] play policy (mcts.py:154-176) */
+  int32_t* latent;      /* [B][n_sims+1] moves of the last simulation's path (mcts.py:79-86) */
+  int32_t* latent_len;  /* [B] */
+  int32_t* sel_steps;   /* [B] total selection steps (sum of depths), for byte accounting */
+} mzh_search_args;
+
+int mzh_search(mzh_engine* eng, const mzh_search_args* args, mzh_stream stream);
+int mzh_search_replay(mzh_engine* eng, const mzh_search_args* args, mzh_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MZH_ABI_H_ */

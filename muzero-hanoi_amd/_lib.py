@@ -1,0 +1,108 @@
+"""ctypes binding of libmzh.so (C ABI: include/mzh.h).
+
+torch is imported first so the process has exactly one HIP runtime: libmzh.so's
+DT_NEEDED libamdhip64.so.7 then resolves to the copy torch already loaded, and device pointers /
+streams from torch are valid inside the library.  There is no fallback: if the library is missing
+or has no device, every call raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede loading libmzh.so, see above)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmzh.so")
+
+MZH_OK = 0
+MZH_ERR_ARG = -1
+MZH_ERR_HIP = -2
+MZH_ERR_CAPACITY = -3
+MZH_ERR_STATE = -4
+MZH_ERR_TEMPERATURE = -5
+MZH_FLAG_NP1_UCB = 1
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+
+
+class SearchArgs(ctypes.Structure):
+    """mirror of struct mzh_search_args (include/mzh.h)"""
+    _fields_ = [
+        ("B", _i32), ("n_sims", _i32), ("discount", ctypes.c_double), ("eps", ctypes.c_double),
+        ("temperature", ctypes.c_double), ("deterministic", _i32), ("flags", ctypes.c_uint32),
+        ("obs", _vp), ("noise", _vp), ("tie_idx", _vp), ("action_u", _vp), ("minmax_in", _vp),
+        ("rp_root_pi", _vp), ("rp_pi", _vp), ("rp_reward", _vp), ("rp_value", _vp),
+        ("visits", _vp), ("root_q", _vp), ("minmax_out", _vp), ("extra_ties", _vp), ("action", _vp),
+        ("pi", _vp), ("latent", _vp), ("latent_len", _vp), ("sel_steps", _vp),
+    ]
+
+
+# name -> (restype, argtypes); every symbol include/mzh.h declares
+SIGNATURES = {
+    "mzh_abi_version": (ctypes.c_int, []),
+    "mzh_last_error": (ctypes.c_char_p, []),
+    "mzh_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "mzh_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.POINTER(_vp)]),
+    "mzh_destroy": (ctypes.c_int, [_vp]),
+    "mzh_weights_size": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
+    "mzh_load_weights": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
+    "mzh_env_step": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int] + [_vp] * 10 + [_vp]),
+    "mzh_legal_mask": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp]),
+    "mzh_encode_obs": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp]),
+    "mzh_hanoi_solver": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp]),
+    "mzh_initial_inference": (ctypes.c_int, [_vp, ctypes.c_int] + [_vp] * 7 + [_vp]),
+    "mzh_recurrent_inference": (ctypes.c_int, [_vp, ctypes.c_int] + [_vp] * 9 + [_vp]),
+    "mzh_search": (ctypes.c_int, [_vp, ctypes.POINTER(SearchArgs), _vp]),
+    "mzh_search_replay": (ctypes.c_int, [_vp, ctypes.POINTER(SearchArgs), _vp]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libmzh.so (once). Raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m muzero_hanoi_amd.build` "
+                               "(there is no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.mzh_abi_version() != 1:
+            raise RuntimeError("libmzh.so ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def last_error():
+    msg = lib().mzh_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(status, what):
+    """Map a status code to the reference's exception types."""
+    if status == MZH_OK:
+        return
+    msg = f"{what}: {last_error()}"
+    if status in (MZH_ERR_ARG, MZH_ERR_TEMPERATURE):
+        raise ValueError(msg)
+    raise RuntimeError(msg)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    st = lib().mzh_device_count(ctypes.byref(n))
+    return n.value if st == MZH_OK else 0
+
+
+def ptr(t):
+    """device pointer of a tensor (None -> NULL)"""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,353 @@
+// mzh_api.hip -- C ABI (include/mzh.h) over the gfx950 kernels.  No exceptions cross the ABI;
+// every entry point returns a status and records a thread-local message.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/mzh.h"
+#include "mzh_env_kernels.h"
+#include "mzh_internal.h"
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+static int hip_fail(hipError_t e, const char* what) {
+  return fail(MZH_ERR_HIP, "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+}
+
+#define HIP_OK(expr)                                   \
+  do {                                                 \
+    hipError_t e_ = (expr);                            \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr);  \
+  } while (0)
+
+// RAII: run on the engine's device, restore the caller's current device afterwards
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int dev) {
+    err = hipGetDevice(&prev);
+    if (err == hipSuccess && prev != dev) err = hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+struct mzh_engine {
+  int device = 0;
+  int n_disks = 0, max_sims = 0, max_roots = 0, support = 33;
+  int in_dim = 0, kin = 0, E = 0;
+  void* wbuf = nullptr;
+  bool loaded = false;
+  MzhNet net{};
+  unsigned char* tree = nullptr;
+  float* htree = nullptr;
+  double* table = nullptr;
+};
+
+extern "C" int mzh_abi_version(void) { return MZH_ABI_VERSION; }
+extern "C" const char* mzh_last_error(void) { return g_err.c_str(); }
+
+extern "C" int mzh_device_count(int* count) {
+  if (!count) return fail(MZH_ERR_ARG, "count is NULL");
+  hipError_t e = hipGetDeviceCount(count);
+  if (e != hipSuccess) {
+    *count = 0;
+    return hip_fail(e, "hipGetDeviceCount");
+  }
+  return MZH_OK;
+}
+
+static size_t canonical_size(int in_dim, int support) {
+  const size_t H = MZH_LATENT, F = MZH_HIDDEN, A = MZH_ACTIONS;
+  size_t s = 0;
+  s += F * in_dim + F + H * F + H;
+  s += F * (H + A) + F + H * F + H;
+  s += F * H + F + (size_t)support * F + support;
+  s += F * H + F + A * F + A;
+  s += F * H + F + (size_t)support * F + support;
+  return s;
+}
+
+extern "C" int mzh_weights_size(int n_disks, int support, size_t* n_floats) {
+  if (n_disks < 1 || n_disks > 16 || (support != 33 && support != 1) || !n_floats)
+    return fail(MZH_ERR_ARG, "bad n_disks=%d / support=%d", n_disks, support);
+  *n_floats = canonical_size(3 * n_disks, support);
+  return MZH_OK;
+}
+
+extern "C" int mzh_create(int device, int n_disks, int max_sims, int max_roots, int support, mzh_engine** out) {
+  if (!out) return fail(MZH_ERR_ARG, "out is NULL");
+  *out = nullptr;
+  if (n_disks < 1 || n_disks > 16) return fail(MZH_ERR_ARG, "n_disks must be in [1,16], got %d", n_disks);
+  if (max_sims < 0 || max_sims > 32000) return fail(MZH_ERR_ARG, "max_sims must be in [0,32000], got %d", max_sims);
+  if (max_roots < 1) return fail(MZH_ERR_ARG, "max_roots must be >= 1, got %d", max_roots);
+  if (support != 33 && support != 1) return fail(MZH_ERR_ARG, "support must be 33 or 1, got %d", support);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MZH_ERR_HIP, "no HIP device available");
+  if (device < 0 || device >= ndev) return fail(MZH_ERR_ARG, "device %d out of range (%d devices)", device, ndev);
+  DeviceGuard g(device);
+  if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+  mzh_engine* eng = new mzh_engine();
+  eng->device = device;
+  eng->n_disks = n_disks;
+  eng->max_sims = max_sims;
+  eng->max_roots = max_roots;
+  eng->support = support;
+  eng->in_dim = 3 * n_disks;
+  eng->kin = ((eng->in_dim + 15) / 16) * 16;
+  eng->E = max_sims + 1;
+  const size_t nblk = (size_t)max_roots * eng->E;
+  hipError_t e = hipMalloc(&eng->tree, nblk * 160);
+  if (e == hipSuccess) e = hipMalloc(&eng->htree, nblk * MZH_LATENT * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&eng->table, sizeof(double) * (size_t)(max_sims + 2));
+  if (e != hipSuccess) {
+    mzh_destroy(eng);
+    return hip_fail(e, "hipMalloc (engine workspace)");
+  }
+  // UCB table on the host with libm, exactly the reference's python expression (node.py:114-121)
+  std::vector<double> t(max_sims + 2);
+  for (int n = 0; n < max_sims + 2; ++n) t[n] = (log((double)(n + 19652 + 1) / 19652.0) + 1.25) * sqrt((double)n);
+  e = hipMemcpy(eng->table, t.data(), sizeof(double) * t.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    mzh_destroy(eng);
+    return hip_fail(e, "hipMemcpy (ucb table)");
+  }
+  *out = eng;
+  return MZH_OK;
+}
+
+extern "C" int mzh_destroy(mzh_engine* eng) {
+  if (!eng) return MZH_OK;
+  DeviceGuard g(eng->device);
+  if (eng->tree) (void)hipFree(eng->tree);
+  if (eng->htree) (void)hipFree(eng->htree);
+  if (eng->table) (void)hipFree(eng->table);
+  if (eng->wbuf) (void)hipFree(eng->wbuf);
+  delete eng;
+  return MZH_OK;
+}
+
+// ---- weight packing: torch [N][K] -> MFMA fragment tiles (see MzhLayer in mzh_device.h) ----
+struct PackedLayer {
+  size_t woff = 0, boff = 0;  // float offsets into the device buffer
+  int kb = 0, nt = 0;
+};
+
+static PackedLayer pack_layer(std::vector<float>& buf, const float* W, const float* b, int N, int K, int ldw) {
+  PackedLayer L;
+  L.nt = (N + 15) / 16;
+  L.kb = (K + 15) / 16;
+  while (buf.size() % 4) buf.push_back(0.0f);
+  L.woff = buf.size();
+  buf.resize(buf.size() + (size_t)L.nt * L.kb * 64 * 4, 0.0f);
+  float* dst = buf.data() + L.woff;
+  for (int nt = 0; nt < L.nt; ++nt)
+    for (int kb = 0; kb < L.kb; ++kb)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 4; ++j) {
+          const int n = 16 * nt + (lane & 15);
+          const int k = 16 * kb + 4 * j + (lane >> 4);
+          dst[(((size_t)nt * L.kb + kb) * 64 + lane) * 4 + j] = (n < N && k < K) ? W[(size_t)n * ldw + k] : 0.0f;
+        }
+  while (buf.size() % 4) buf.push_back(0.0f);
+  L.boff = buf.size();
+  buf.resize(buf.size() + (size_t)L.nt * 16, 0.0f);
+  for (int n = 0; n < N; ++n) buf[L.boff + n] = b[n];
+  return L;
+}
+
+extern "C" int mzh_load_weights(mzh_engine* eng, const float* flat, size_t n_floats) {
+  if (!eng || !flat) return fail(MZH_ERR_ARG, "engine or weights NULL");
+  const size_t want = canonical_size(eng->in_dim, eng->support);
+  if (n_floats != want) return fail(MZH_ERR_ARG, "weights: expected %zu floats, got %zu", want, n_floats);
+  const int H = MZH_LATENT, F = MZH_HIDDEN, A = MZH_ACTIONS, in = eng->in_dim, sup = eng->support;
+  const float* p = flat;
+  auto take = [&](size_t n) { const float* q = p; p += n; return q; };
+  const float *rep0w = take((size_t)F * in), *rep0b = take(F), *rep2w = take((size_t)H * F), *rep2b = take(H);
+  const float *dyn0w = take((size_t)F * (H + A)), *dyn0b = take(F), *dyn2w = take((size_t)H * F), *dyn2b = take(H);
+  const float *rwd0w = take((size_t)F * H), *rwd0b = take(F), *rwd2w = take((size_t)sup * F), *rwd2b = take(sup);
+  const float *pol0w = take((size_t)F * H), *pol0b = take(F), *pol2w = take((size_t)A * F), *pol2b = take(A);
+  const float *val0w = take((size_t)F * H), *val0b = take(F), *val2w = take((size_t)sup * F), *val2b = take(sup);
+
+  std::vector<float> buf;
+  buf.reserve(200000);
+  PackedLayer L[10];
+  L[0] = pack_layer(buf, rep0w, rep0b, F, in, in);
+  L[1] = pack_layer(buf, rep2w, rep2b, H, F, F);
+  L[2] = pack_layer(buf, dyn0w, dyn0b, F, H, H + A);  // h part only (k < 64)
+  L[3] = pack_layer(buf, dyn2w, dyn2b, H, F, F);
+  L[4] = pack_layer(buf, rwd0w, rwd0b, F, H, H);
+  L[5] = pack_layer(buf, rwd2w, rwd2b, sup, F, F);
+  L[6] = pack_layer(buf, pol0w, pol0b, F, H, H);
+  L[7] = pack_layer(buf, pol2w, pol2b, A, F, F);
+  L[8] = pack_layer(buf, val0w, val0b, F, H, H);
+  L[9] = pack_layer(buf, val2w, val2b, sup, F, F);
+  while (buf.size() % 4) buf.push_back(0.0f);
+  const size_t ohoff = buf.size();
+  buf.resize(buf.size() + (size_t)A * F);
+  for (int a = 0; a < A; ++a)
+    for (int n = 0; n < F; ++n) buf[ohoff + (size_t)a * F + n] = dyn0w[(size_t)n * (H + A) + H + a];
+
+  DeviceGuard g(eng->device);
+  if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+  if (eng->wbuf) {
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipFree(eng->wbuf));
+    eng->wbuf = nullptr;
+    eng->loaded = false;
+  }
+  HIP_OK(hipMalloc(&eng->wbuf, buf.size() * sizeof(float)));
+  HIP_OK(hipMemcpy(eng->wbuf, buf.data(), buf.size() * sizeof(float), hipMemcpyHostToDevice));
+  const float* base = static_cast<const float*>(eng->wbuf);
+  auto mk = [&](const PackedLayer& pl) {
+    MzhLayer m;
+    m.w = reinterpret_cast<const float4*>(base + pl.woff);
+    m.b = base + pl.boff;
+    m.kb = pl.kb;
+    m.nt = pl.nt;
+    return m;
+  };
+  MzhNet& n = eng->net;
+  n.rep0 = mk(L[0]); n.rep2 = mk(L[1]); n.dyn0 = mk(L[2]); n.dyn2 = mk(L[3]); n.rwd0 = mk(L[4]);
+  n.rwd2 = mk(L[5]); n.pol0 = mk(L[6]); n.pol2 = mk(L[7]); n.val0 = mk(L[8]); n.val2 = mk(L[9]);
+  n.dyn0_onehot = base + ohoff;
+  n.support = sup;
+  n.in_dim = in;
+  eng->loaded = true;
+  return MZH_OK;
+}
+
+// ---- environment ----
+extern "C" int mzh_env_step(int n_disks, int goal_peg, int max_steps, int B, uint8_t* state, const int32_t* action,
+                            uint8_t* moved, float* obs, int8_t* reward, uint8_t* done, uint8_t* illegal,
+                            int32_t* step_ctr, uint8_t* active, int32_t* err_count, mzh_stream stream) {
+  if (n_disks < 1 || n_disks > 32 || goal_peg < 0 || goal_peg > 2 || B < 0)
+    return fail(MZH_ERR_ARG, "env_step: bad n_disks=%d goal_peg=%d B=%d", n_disks, goal_peg, B);
+  if (B == 0) return MZH_OK;
+  if (!state || !action || !reward || !done || !illegal || !step_ctr || !active)
+    return fail(MZH_ERR_ARG, "env_step: required buffer is NULL");
+  hipError_t e = mzh_launch_env_step(n_disks, goal_peg, max_steps, B, state, action, moved, obs, reward, done, illegal,
+                                     step_ctr, active, err_count, (hipStream_t)stream);
+  return e == hipSuccess ? MZH_OK : hip_fail(e, "env_step launch");
+}
+
+extern "C" int mzh_legal_mask(int n_disks, int B, const uint8_t* state, uint8_t* mask, mzh_stream stream) {
+  if (n_disks < 1 || n_disks > 32 || B < 0 || (B > 0 && (!state || !mask))) return fail(MZH_ERR_ARG, "legal_mask: bad args");
+  if (B == 0) return MZH_OK;
+  hipError_t e = mzh_launch_legal_mask(n_disks, B, state, mask, (hipStream_t)stream);
+  return e == hipSuccess ? MZH_OK : hip_fail(e, "legal_mask launch");
+}
+
+extern "C" int mzh_encode_obs(int n_disks, int B, const uint8_t* state, float* obs, mzh_stream stream) {
+  if (n_disks < 1 || n_disks > 32 || B < 0 || (B > 0 && (!state || !obs))) return fail(MZH_ERR_ARG, "encode_obs: bad args");
+  if (B == 0) return MZH_OK;
+  hipError_t e = mzh_launch_encode_obs(n_disks, B, state, obs, (hipStream_t)stream);
+  return e == hipSuccess ? MZH_OK : hip_fail(e, "encode_obs launch");
+}
+
+extern "C" int mzh_hanoi_solver(int n_disks, int goal_peg, int B, const uint8_t* state, int32_t* moves, mzh_stream stream) {
+  if (n_disks < 1 || n_disks > 30 || goal_peg < 0 || goal_peg > 2 || B < 0 || (B > 0 && (!state || !moves)))
+    return fail(MZH_ERR_ARG, "hanoi_solver: bad args");
+  if (B == 0) return MZH_OK;
+  hipError_t e = mzh_launch_hanoi_solver(n_disks, goal_peg, B, state, moves, (hipStream_t)stream);
+  return e == hipSuccess ? MZH_OK : hip_fail(e, "hanoi_solver launch");
+}
+
+// ---- inference ----
+static int pick_rows(int B) { return B >= 256 * 32 ? 32 : 16; }
+
+extern "C" int mzh_initial_inference(mzh_engine* eng, int B, const float* obs, float* h, float* reward, float* pi,
+                                     float* value, float* policy_logits, float* value_logits, mzh_stream stream) {
+  if (!eng) return fail(MZH_ERR_ARG, "engine NULL");
+  if (!eng->loaded) return fail(MZH_ERR_STATE, "weights not loaded");
+  if (B < 0 || (B > 0 && (!obs || !h))) return fail(MZH_ERR_ARG, "initial_inference: bad args");
+  if (B == 0) return MZH_OK;
+  DeviceGuard g(eng->device);
+  if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+  MzhInferParams p{};
+  p.B = B; p.in_dim = eng->in_dim; p.kin = eng->kin; p.x = obs; p.h = h; p.reward = reward; p.pi = pi;
+  p.value = value; p.policy_logits = policy_logits; p.value_logits = value_logits;
+  hipError_t e = mzh_launch_infer(pick_rows(B), false, eng->net, p, (hipStream_t)stream);
+  return e == hipSuccess ? MZH_OK : hip_fail(e, "initial_inference launch");
+}
+
+extern "C" int mzh_recurrent_inference(mzh_engine* eng, int B, const float* h_in, const int32_t* action, float* h,
+                                       float* reward, float* pi, float* value, float* policy_logits,
+                                       float* value_logits, float* reward_logits, mzh_stream stream) {
+  if (!eng) return fail(MZH_ERR_ARG, "engine NULL");
+  if (!eng->loaded) return fail(MZH_ERR_STATE, "weights not loaded");
+  if (B < 0 || (B > 0 && (!h_in || !action || !h))) return fail(MZH_ERR_ARG, "recurrent_inference: bad args");
+  if (B == 0) return MZH_OK;
+  DeviceGuard g(eng->device);
+  if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+  MzhInferParams p{};
+  p.B = B; p.in_dim = eng->in_dim; p.kin = eng->kin; p.x = h_in; p.action = action; p.h = h; p.reward = reward;
+  p.pi = pi; p.value = value; p.policy_logits = policy_logits; p.value_logits = value_logits;
+  p.reward_logits = reward_logits;
+  hipError_t e = mzh_launch_infer(pick_rows(B), true, eng->net, p, (hipStream_t)stream);
+  return e == hipSuccess ? MZH_OK : hip_fail(e, "recurrent_inference launch");
+}
+
+// ---- search ----
+static const size_t kMaxLds = 163840;
+
+static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream stream, bool replay) {
+  if (!eng || !a) return fail(MZH_ERR_ARG, "engine or args NULL");
+  if (a->B < 0 || a->n_sims < 0) return fail(MZH_ERR_ARG, "B=%d n_sims=%d", a->B, a->n_sims);
+  if (a->B > eng->max_roots) return fail(MZH_ERR_CAPACITY, "B=%d > max_roots=%d", a->B, eng->max_roots);
+  if (a->n_sims > eng->max_sims) return fail(MZH_ERR_CAPACITY, "n_sims=%d > max_sims=%d", a->n_sims, eng->max_sims);
+  if (!(a->temperature >= 0.0 && a->temperature <= 1.0))
+    return fail(MZH_ERR_TEMPERATURE, "Expect `temperature` to be in the range [0.0, 1.0], got %g", a->temperature);
+  if (a->B == 0) return MZH_OK;
+  if (!a->visits) return fail(MZH_ERR_ARG, "visits output is required");
+  if (replay) {
+    if (!a->rp_root_pi || (a->n_sims > 0 && (!a->rp_pi || !a->rp_reward || !a->rp_value)))
+      return fail(MZH_ERR_ARG, "replay search needs rp_root_pi / rp_pi / rp_reward / rp_value");
+  } else {
+    if (!eng->loaded) return fail(MZH_ERR_STATE, "weights not loaded");
+    if (!a->obs) return fail(MZH_ERR_ARG, "obs is required");
+  }
+  if (!a->deterministic && !a->action_u && a->action)
+    return fail(MZH_ERR_ARG, "stochastic action selection needs action_u");
+  int R = pick_rows(a->B);
+  if (mzh_search_smem_bytes(R, a->n_sims) > kMaxLds) R = 16;
+  if (mzh_search_smem_bytes(R, a->n_sims) > kMaxLds)
+    return fail(MZH_ERR_CAPACITY, "n_sims=%d exceeds the LDS path budget", a->n_sims);
+  DeviceGuard g(eng->device);
+  if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+  MzhSearchParams p{};
+  p.B = a->B; p.S = a->n_sims; p.E = eng->E; p.in_dim = eng->in_dim; p.kin = eng->kin;
+  p.deterministic = a->deterministic; p.np1 = (a->flags & MZH_FLAG_NP1_UCB) ? 1 : 0;
+  p.discount = a->discount; p.eps = a->eps; p.temperature = a->temperature;
+  p.obs = a->obs; p.noise = a->noise; p.tie_idx = a->tie_idx; p.action_u = a->action_u; p.minmax_in = a->minmax_in;
+  p.rp_root_pi = a->rp_root_pi; p.rp_pi = a->rp_pi; p.rp_reward = a->rp_reward; p.rp_value = a->rp_value;
+  p.tree = eng->tree; p.htree = eng->htree; p.table = eng->table;
+  p.visits = a->visits; p.root_q = a->root_q; p.minmax_out = a->minmax_out; p.extra_ties = a->extra_ties;
+  p.action = a->action; p.pi = a->pi; p.latent = a->latent; p.latent_len = a->latent_len; p.sel_steps = a->sel_steps;
+  hipError_t e = mzh_launch_search(R, replay, eng->net, p, (hipStream_t)stream);
+  return e == hipSuccess ? MZH_OK : hip_fail(e, "search launch");
+}
+
+extern "C" int mzh_search(mzh_engine* eng, const mzh_search_args* args, mzh_stream stream) {
+  return search_common(eng, args, stream, false);
+}
+
+extern "C" int mzh_search_replay(mzh_engine* eng, const mzh_search_args* args, mzh_stream stream) {
+  return search_common(eng, args, stream, true);
+}

@@ -1,0 +1,127 @@
+"""MCTS drop-in (reference: MCTS/mcts.py:8-176, MCTS/node.py, MCTS/utils_mcts.py).
+
+`MCTS.run_mcts(state, network, temperature, deterministic)` keeps the reference's signature,
+return types, RNG consumption (global legacy NumPy stream, see rng.py), MinMaxStats persistence
+across calls on one instance (mcts.py:23) and `return_latent_actions`.  The whole search -- root
+inference, every simulation's select / MLP expansion / backup, and the play policy -- is one
+fused libmzh kernel launch on the GPU (mzh_search).
+
+`MCTS.run_batch(states, ...)` runs B independent searches in one launch (each root with its own
+MinMaxStats, i.e. B fresh single-root searches), the form the bench and batched self-play use.
+"""
+import warnings
+
+import numpy as np
+import torch
+
+from . import rng as _rng
+from .networks import engine_for
+
+
+class MinMaxStats(object):
+    """utils_mcts.py:1-16 (host mirror; the device carries the same two doubles)."""
+
+    def __init__(self, min_value_bound=None, max_value_bound=None):
+        self.maximum = min_value_bound if min_value_bound else -float("inf")
+        self.minimum = max_value_bound if max_value_bound else float("inf")
+
+    def update(self, value):
+        self.maximum = max(self.maximum, value)
+        self.minimum = min(self.minimum, value)
+
+    def normalize(self, value):
+        if self.maximum > self.minimum:
+            return (value - self.minimum) / (self.maximum - self.minimum)
+        return value
+
+
+class MCTS:
+    def __init__(self, discount, root_dirichlet_alpha, n_simulations, batch_s, device, h_dim=64, clip_grad=True,
+                 root_exploration_eps=0.25, known_bounds=[]):
+        self.min_max_stats = MinMaxStats()
+        self.pb_c_base = 19652  # baked into the kernel's UCB table (mzh_create)
+        self.pb_c_init = 1.25
+        self.discount = discount
+        self.root_dirichlet_alpha = root_dirichlet_alpha
+        self.root_exploration_eps = root_exploration_eps
+        self.n_simulations = n_simulations
+        self.batch_s = batch_s
+        self.dev = device
+        self.latent_actions = []
+        self.np1_ucb = False  # True: NumPy-1.x UCB rounding (the reference's numpy==1.25.2 pin)
+        self.last_extra_ties = 0
+
+    # ------------------------------------------------------------------ reference API
+    def run_mcts(self, state, network, temperature, deterministic):
+        """mcts.py:34-126 -> (action int, pi np.float64[6], root Q float)."""
+        if self.pb_c_base != 19652 or self.pb_c_init != 1.25:
+            raise NotImplementedError("libmzh bakes pb_c_base=19652, pb_c_init=1.25 (mcts.py:24-25)")
+        S = int(self.n_simulations)
+        noise, tie, u = _rng.predraw(1, deterministic=deterministic, alpha=self.root_dirichlet_alpha,
+                                     eps=self.root_exploration_eps)
+        if not 0.0 <= temperature <= 1.0:  # raised after the search's draws, like mcts.py:163-166
+            raise ValueError(f"Expect `temperature` to be in the range [0.0, 1.0], got {temperature}")
+        eng = engine_for(network, S, 1)
+        dev = eng.device
+        obs = torch.as_tensor(np.asarray(state)).to(dev, torch.float32).reshape(1, -1)
+        mm = torch.tensor([[self.min_max_stats.maximum, self.min_max_stats.minimum]], dtype=torch.float64, device=dev)
+        t = lambda a: None if a is None else torch.from_numpy(np.asarray(a)).to(dev)
+        out = eng.search(S, obs=obs, tie_idx=t(tie), noise=t(noise), action_u=t(u), minmax_in=mm,
+                         temperature=float(temperature), deterministic=bool(deterministic),
+                         discount=float(self.discount), eps=float(self.root_exploration_eps), np1_ucb=self.np1_ucb)
+        host = {k: v.cpu().numpy() for k, v in out.items() if k != "_keep"}
+        self.min_max_stats.maximum = float(host["minmax"][0, 0])
+        self.min_max_stats.minimum = float(host["minmax"][0, 1])
+        L = int(host["latent_len"][0])
+        self.latent_actions = [torch.tensor([int(m)], dtype=torch.long, device=self.dev) for m in host["latent"][0, :L]]
+        self.last_extra_ties = int(host["extra_ties"][0])
+        if self.last_extra_ties:
+            warnings.warn("search met an argmax tie beyond the root's first selection: the NumPy RNG stream "
+                          "now differs from the reference's", RuntimeWarning)
+        return int(host["action"][0]), host["pi"][0].astype(np.float64), float(host["root_q"][0])
+
+    def return_latent_actions(self):
+        return self.latent_actions
+
+    def add_dirichlet_noise(self, prob, eps=0.25, alpha=0.25):
+        """mcts.py:132-152 (host form, for callers that use it directly)."""
+        if not isinstance(prob, np.ndarray) or prob.dtype not in (np.float32, np.float64):
+            raise ValueError(f"Expect `prob` to be a numpy.array, got {prob}")
+        noise = np.random.dirichlet(np.ones_like(prob) * alpha)
+        return (1 - eps) * prob + eps * noise
+
+    def generate_play_policy(self, visits_count, temperature):
+        """mcts.py:154-176 (host form; the search kernel computes the same policy on device)."""
+        if not 0.0 <= temperature <= 1.0:
+            raise ValueError(f"Expect `temperature` to be in the range [0.0, 1.0], got {temperature}")
+        visits_count = np.asarray(visits_count, dtype=np.int64)
+        if temperature > 0.0:
+            visits_count = np.power(visits_count, max(1.0, min(5.0, 1.0 / temperature)))
+        return visits_count / np.sum(visits_count)
+
+    # ------------------------------------------------------------------ batched form
+    def run_batch(self, states, network, temperature, deterministic, *, legacy_rng=True, seed=None, minmax=None,
+                  out=None):
+        """B independent run_mcts calls in one kernel launch.
+
+        states: [B, 3N] observations (numpy or tensor).  With legacy_rng the draws come from the
+        global NumPy stream in the order B sequential run_mcts calls would consume them (each
+        root with a fresh MinMaxStats, unless `minmax` [B,2] is given); otherwise a vectorised
+        Generator(seed) is used.  Returns device tensors (visits, action, pi, root_q, minmax, ...).
+        """
+        S = int(self.n_simulations)
+        obs = torch.as_tensor(states)
+        B = obs.shape[0]
+        if legacy_rng:
+            noise, tie, u = _rng.predraw(B, deterministic=deterministic, alpha=self.root_dirichlet_alpha,
+                                         eps=self.root_exploration_eps)
+        else:
+            noise, tie, u = _rng.synthetic_draws(B, deterministic=deterministic, alpha=self.root_dirichlet_alpha,
+                                                 eps=self.root_exploration_eps, seed=seed or 0)
+        eng = engine_for(network, S, B)
+        dev = eng.device
+        t = lambda a: None if a is None else torch.as_tensor(a).to(dev)
+        return eng.search(S, obs=obs.to(dev, torch.float32), tie_idx=t(tie), noise=t(noise), action_u=t(u),
+                          minmax_in=t(minmax), temperature=float(temperature), deterministic=bool(deterministic),
+                          discount=float(self.discount), eps=float(self.root_exploration_eps),
+                          np1_ucb=self.np1_ucb, out=out)

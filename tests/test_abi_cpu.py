@@ -1,0 +1,130 @@
+"""CPU-side checks of the boundary: libmzh.so loads, exports every symbol include/mzh.h declares,
+the ctypes struct mirrors the C struct, and host logic behaves (no compute calls without a GPU)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "mzh.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(mzh_\w+)\(", txt, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from muzero_hanoi_amd import build
+
+    build.build()
+    from muzero_hanoi_amd import _lib
+
+    return _lib
+
+
+def test_library_exports_every_declared_symbol(lib):
+    syms = declared_symbols()
+    assert len(syms) >= 15
+    L = lib.lib()
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(lib.SIGNATURES), "ctypes signature table out of sync with include/mzh.h"
+    assert L.mzh_abi_version() == 1
+
+
+def test_search_args_layout_matches_header(lib):
+    # the C struct: 2 x int32, 3 x double, int32, uint32, 18 pointers
+    assert ctypes.sizeof(lib.SearchArgs) == 8 + 24 + 8 + 18 * 8
+    assert lib.SearchArgs.obs.offset == 40
+    n_ptr_fields = len(re.findall(r"^\s+(?:const\s+)?\w+\*\s+\w+;", open(HEADER).read(), re.M))
+    assert n_ptr_fields == 18
+
+
+def test_errors_without_device_are_loud(lib):
+    if torch.cuda.is_available():
+        pytest.skip("host without GPU only")
+    L = lib.lib()
+    h = ctypes.c_void_p()
+    st = L.mzh_create(0, 4, 10, 10, 33, ctypes.byref(h))
+    assert st == lib.MZH_ERR_HIP and not h.value
+    assert "device" in lib.last_error()
+    assert lib.device_count() == 0
+    from muzero_hanoi_amd import engine
+
+    with pytest.raises(RuntimeError):
+        engine.Engine(4, 10, 10)
+
+
+def test_argument_validation_without_device(lib):
+    L = lib.lib()
+    n = ctypes.c_size_t()
+    assert L.mzh_weights_size(4, 33, ctypes.byref(n)) == 0
+    assert n.value == 122824  # 122,824 params at N=4
+    assert L.mzh_weights_size(3, 1, ctypes.byref(n)) == 0
+    assert L.mzh_weights_size(0, 33, ctypes.byref(n)) == lib.MZH_ERR_ARG
+    assert L.mzh_weights_size(4, 7, ctypes.byref(n)) == lib.MZH_ERR_ARG
+    assert L.mzh_create(0, 0, 10, 10, 33, ctypes.byref(ctypes.c_void_p())) == lib.MZH_ERR_ARG
+    assert L.mzh_env_step(0, 2, 10, 1, *([None] * 11)) == lib.MZH_ERR_ARG
+    assert L.mzh_search(None, None, None) == lib.MZH_ERR_ARG
+    with pytest.raises(ValueError):
+        lib.check(lib.MZH_ERR_TEMPERATURE, "x")
+    with pytest.raises(RuntimeError):
+        lib.check(lib.MZH_ERR_HIP, "x")
+
+
+def test_weight_flattening_matches_state_dict_order():
+    from muzero_hanoi_amd import engine
+    from muzero_hanoi_amd.networks import MuZeroNet
+    from oracle import oracle as orc
+
+    torch.manual_seed(0)
+    net = MuZeroNet(12, 6, 0.002, "cpu", TD_return=True)
+    flat = engine.flat_weights(net.state_dict())
+    assert flat.size == 122824
+    assert engine.WEIGHT_KEYS == orc.WEIGHT_KEYS
+    # same seed -> the reference's initial weights (fixture from the reference itself)
+    g = np.load(os.path.join(ROOT, "tests", "golden", "weights_N4_s0.npz"))
+    for k in engine.WEIGHT_KEYS:
+        assert np.array_equal(net.state_dict()[k].numpy(), g[k]), k
+
+
+def test_dropin_torch_paths_match_reference_fixture():
+    """MuZeroNet's torch methods (training/analysis path, not the HIP hot path) reproduce the
+    reference's represent/prediction outputs on its own weights."""
+    from muzero_hanoi_amd.networks import MuZeroNet
+
+    torch.manual_seed(0)
+    net = MuZeroNet(12, 6, 0.002, "cpu", TD_return=True)
+    g = np.load(os.path.join(ROOT, "tests", "golden", "mlp_N4_s0.npz"))
+    with torch.no_grad():
+        h = net.represent(torch.tensor(g["x"]))
+        pl, v = net.prediction(h)
+    # batched torch GEMMs round differently from the reference's batch-1 calls: tolerances
+    np.testing.assert_allclose(h.numpy(), g["ii_h"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(pl.numpy(), g["ii_policy_logits"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(v.numpy()[:, 0], g["ii_value"], atol=2e-3, rtol=0)
+
+
+def test_rng_predraw_consumes_like_reference():
+    from muzero_hanoi_amd import rng
+
+    np.random.seed(3)
+    a = rng.predraw(5, deterministic=False, alpha=0.25)
+    np.random.seed(3)
+    manual = []
+    for _ in range(5):
+        d = np.random.dirichlet(np.ones(6, np.float32) * 0.25)
+        t = np.random.choice(np.arange(6))
+        u = np.random.random_sample()
+        manual.append((d, t, u))
+    assert np.array_equal(a[0], np.array([m[0] for m in manual]))
+    assert np.array_equal(a[1], np.array([m[1] for m in manual]))
+    assert np.array_equal(a[2], np.array([m[2] for m in manual]))
+    n, t, u = rng.predraw(3, deterministic=True, alpha=0.25)
+    assert n is None and u is None and t.shape == (3,)

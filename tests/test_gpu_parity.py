@@ -1,0 +1,234 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the reference fixtures.
+
+Bars (north_star): env transitions and visit counts bit-exact; logits within 1e-5 of the
+reference (torch-CPU); against the oracle (same fp32 op order) the MLP is expected bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, REPLAY_CASES, golden
+from test_oracle_golden import _index, _states, replay_draws, replay_inputs
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def mzh():
+    from muzero_hanoi_amd import _lib, engine
+
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    _lib.lib()
+    return engine
+
+
+def _engine(mzh, n, S, B, support=33, weights=None):
+    eng = mzh.Engine(n, S, B, support)
+    if weights is not None:
+        eng.load_weights(weights)
+    return eng
+
+
+def _weights(oracle, name):
+    w, in_dim, sup = oracle.load_weights_npz(f"{GOLDEN}/{name}.npz")
+    return oracle.flat_weights(w), in_dim, sup
+
+
+# ------------------------------------------------------------------------------------ env
+@pytest.mark.parametrize("n", [3, 4, 7])
+def test_env_step_exhaustive(mzh, n):
+    g = golden(f"env_N{n}.npz")
+    states = _states(n)
+    S = len(states)
+    st = torch.tensor(np.repeat(states, 6, axis=0), device=DEV)
+    act = torch.tensor(np.tile(np.arange(6), S), dtype=torch.int32, device=DEV)
+    ctr = torch.zeros(S * 6, dtype=torch.int32, device=DEV)
+    active = torch.ones(S * 6, dtype=torch.uint8, device=DEV)
+    moved = torch.empty_like(st)
+    obs = torch.empty((S * 6, 3 * n), dtype=torch.float32, device=DEV)
+    rew, done, ill = mzh.env_step(n, 10**9, st, act, ctr, active, moved=moved, obs=obs)
+    torch.cuda.synchronize()
+    st, moved, obs = st.cpu().numpy(), moved.cpu().numpy(), obs.cpu().numpy()
+    rew, done, ill = rew.cpu().numpy(), done.cpu().numpy(), ill.cpu().numpy()
+    code_to_rwd = {0: 0.0, 1: 100.0, -1: -100 / 1000}
+    for i in range(S):
+        for a in range(6):
+            k = i * 6 + a
+            assert _index(st[k]) == g["next_state"][i, a]
+            assert _index(moved[k]) == g["moved_state"][i, a]
+            assert code_to_rwd[int(rew[k])] == g["reward"][i, a]
+            assert done[k] == g["done"][i, a] and ill[k] == g["illegal"][i, a]
+            want = np.zeros(3 * n, np.float32)
+            want[np.arange(n) * 3 + moved[k]] = 1
+            assert np.array_equal(obs[k], want)
+    mask = mzh.legal_mask(n, torch.tensor(states, device=DEV)).cpu().numpy()
+    assert np.array_equal(mask, (g["legal"].astype(np.int64) << np.arange(6)).sum(1))
+    sol = mzh.hanoi_solver_batch(n, torch.tensor(states, device=DEV)).cpu().numpy()
+    assert np.array_equal(sol, golden(f"solver_N{n}.npz")["moves"])
+    sol0 = mzh.hanoi_solver_batch(n, torch.tensor(states, device=DEV), goal_peg=0).cpu().numpy()
+    assert np.array_equal(sol0, golden(f"solver_N{n}.npz")["moves_goal0"])
+
+
+def test_env_maxsteps_and_assert(mzh):
+    g = golden("env_maxsteps.npz")
+    for row in g["rows"]:
+        n, max_steps, _, before, ctr_before, a, moved, after, rwd, done, ill, ctr_after, rc = [int(v) if i != 8 else v for i, v in enumerate(row)]
+        st = torch.tensor(_states(n)[before][None], device=DEV)
+        mv = torch.empty_like(st)
+        ctr = torch.tensor([ctr_before], dtype=torch.int32, device=DEV)
+        active = torch.ones(1, dtype=torch.uint8, device=DEV)
+        r, d, il = mzh.env_step(n, max_steps, st, torch.tensor([a], dtype=torch.int32, device=DEV), ctr, active, moved=mv)
+        assert _index(st[0].cpu().numpy()) == after and _index(mv[0].cpu().numpy()) == moved
+        assert {0: 0.0, 1: 100.0, -1: -0.1}[int(r.item())] == rwd
+        assert (int(d.item()), int(il.item()), int(ctr.item()), int(active.item())) == (done, ill, ctr_after, rc)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    st = torch.zeros((2, 3), dtype=torch.uint8, device=DEV)
+    r, d, il = mzh.env_step(3, 10, st, torch.tensor([0, 9], dtype=torch.int32, device=DEV),
+                            torch.zeros(2, dtype=torch.int32, device=DEV),
+                            torch.tensor([0, 1], dtype=torch.uint8, device=DEV), err=err)
+    assert err.item() == 2 and r.tolist() == [-2, -2]
+
+
+# ------------------------------------------------------------------------------------ MLP
+@pytest.mark.parametrize("name", ["mlp_N3_s0", "mlp_N4_s0", "mlp_N4_s1", "mlp_N7_s0", "mlp_N3_s0_mc"])
+def test_mlp_vs_reference_and_oracle(mzh, oracle, name):
+    g = golden(name + ".npz")
+    flat, in_dim, sup = _weights(oracle, name.replace("mlp_", "weights_"))
+    n = in_dim // 3
+    eng = _engine(mzh, n, 4, 64, sup, flat)
+    ii = {k: v.cpu().numpy() for k, v in eng.initial_inference(torch.tensor(g["x"], device=DEV)).items()}
+    ri = {k: v.cpu().numpy() for k, v in eng.recurrent_inference(torch.tensor(g["h_in"], device=DEV),
+                                                                  torch.tensor(g["a_in"], device=DEV)).items()}
+    # vs the reference (torch-CPU): logits within 1e-5 (north_star); transformed scalars 2e-3
+    np.testing.assert_allclose(ii["policy_logits"], g["ii_policy_logits"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(ii["value_logits"], g["ii_value_logits"].reshape(ii["value_logits"].shape), atol=1e-5, rtol=0)
+    np.testing.assert_allclose(ii["h"], g["ii_h"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(ii["pi"], g["ii_pi"], atol=1e-6, rtol=0)
+    np.testing.assert_allclose(ii["value"], g["ii_value"], atol=2e-3, rtol=0)
+    np.testing.assert_allclose(ri["policy_logits"], g["ri_policy_logits"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(ri["value_logits"], g["ri_value_logits"].reshape(ri["value_logits"].shape), atol=1e-5, rtol=0)
+    np.testing.assert_allclose(ri["reward_logits"], g["ri_rwd_logits"].reshape(ri["reward_logits"].shape), atol=1e-5, rtol=0)
+    np.testing.assert_allclose(ri["h"], g["ri_h"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(ri["value"], g["ri_value"], atol=2e-3, rtol=0)
+    np.testing.assert_allclose(ri["reward"], g["ri_rwd"], atol=2e-3, rtol=0)
+    # vs the oracle: identical fp32 operation order -> identical bits
+    oi = oracle.initial_inference(flat, in_dim, sup, g["x"])
+    orr = oracle.recurrent_inference(flat, in_dim, sup, g["h_in"], g["a_in"])
+    for k in ("h", "pi", "value", "policy_logits", "value_logits"):
+        assert np.array_equal(ii[k], oi[k]), f"initial {k}: max |d| = {np.abs(ii[k] - oi[k]).max()}"
+    for k in ("h", "pi", "value", "reward", "policy_logits", "value_logits", "reward_logits"):
+        assert np.array_equal(ri[k], orr[k]), f"recurrent {k}: max |d| = {np.abs(ri[k] - orr[k]).max()}"
+
+
+@pytest.mark.parametrize("B", [1, 17, 300, 9000])
+def test_mlp_batch_sizes_vs_oracle(mzh, oracle, B):
+    flat, in_dim, sup = _weights(oracle, "weights_N4_s0")
+    rs = np.random.RandomState(B)
+    x = np.zeros((B, 12), np.float32)
+    st = rs.randint(0, 3, (B, 4))
+    x[np.arange(B)[:, None], np.arange(4) * 3 + st] = 1
+    h = rs.uniform(0, 1, (B, 64)).astype(np.float32)
+    a = rs.randint(0, 6, B).astype(np.int32)
+    eng = _engine(mzh, 4, 4, B, 33, flat)
+    ii = eng.initial_inference(torch.tensor(x, device=DEV))
+    ri = eng.recurrent_inference(torch.tensor(h, device=DEV), torch.tensor(a, device=DEV))
+    oi = oracle.initial_inference(flat, in_dim, sup, x)
+    orr = oracle.recurrent_inference(flat, in_dim, sup, h, a)
+    for k in ("h", "pi", "value"):
+        assert np.array_equal(ii[k].cpu().numpy(), oi[k])
+    for k in ("h", "pi", "value", "reward"):
+        assert np.array_equal(ri[k].cpu().numpy(), orr[k])
+
+
+# ------------------------------------------------------------------------------------ search
+def _run_replay_case(mzh, g):
+    S, n = int(g["s"]), int(g["n"])
+    det, T = bool(g["deterministic"]), float(g["temperature"])
+    rp = replay_inputs(g)
+    B = g["obs"].shape[0]
+    eng = _engine(mzh, n, max(S, 1), B, 33 if int(g["td"]) else 1)
+    tt = lambda a, dt=None: None if a is None else torch.tensor(np.asarray(a), dtype=dt, device=DEV)
+    if int(g["shared"]):
+        draws = replay_draws(g)
+        mm = torch.tensor([[-np.inf, np.inf]], dtype=torch.float64, device=DEV)
+        outs = []
+        for b in range(B):
+            noise, tie, u = draws[b]
+            o = eng.search(S, replay={k: tt(v[b:b + 1]) for k, v in dict(root_pi=rp["root_pi"], pi=rp["pi"], reward=rp["rwd"], value=rp["value"]).items()},
+                           tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), minmax_in=mm,
+                           temperature=T, deterministic=det, discount=float(g["discount"]))
+            mm = o["minmax"].clone()
+            outs.append({k: v.cpu().numpy() for k, v in o.items() if k != "_keep"})
+        return {k: np.concatenate([o[k] for o in outs]) for k in outs[0]}
+    noise, tie, u = replay_draws(g)
+    o = eng.search(S, replay=dict(root_pi=tt(rp["root_pi"]), pi=tt(rp["pi"]), reward=tt(rp["rwd"]), value=tt(rp["value"])),
+                   tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=T, deterministic=det,
+                   discount=float(g["discount"]))
+    return {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+
+
+@pytest.mark.parametrize("case", REPLAY_CASES)
+def test_search_replay_bit_exact_vs_reference(mzh, case):
+    g = golden(f"replay_{case}.npz")
+    out = _run_replay_case(mzh, g)
+    assert np.array_equal(out["visits"], g["visits"])
+    assert np.array_equal(out["root_q"], g["rootQ"])
+    assert np.array_equal(out["minmax"][:, 0], g["mm_max"]) and np.array_equal(out["minmax"][:, 1], g["mm_min"])
+    assert np.array_equal(out["pi"], g["pi"])
+    assert np.array_equal(out["action"], g["action"])
+    assert np.all(out["extra_ties"] == 0)
+    for b in range(g["obs"].shape[0]):
+        L = out["latent_len"][b]
+        want = g["latent"][b]
+        assert list(out["latent"][b][:L]) == [int(v) for v in want[want >= 0]]
+
+
+@pytest.mark.parametrize("case", [c for c in REPLAY_CASES if "shared" not in c])
+def test_search_mlp_end_to_end_vs_oracle(mzh, oracle, case):
+    """Full fused search (MLP on MFMA) == oracle search with the same weights, bit for bit."""
+    g = golden(f"replay_{case}.npz")
+    S, n, td = int(g["s"]), int(g["n"]), int(g["td"])
+    flat, in_dim, sup = _weights(oracle, f"weights_N{n}_s{int(g['wseed'])}{'' if td else '_mc'}")
+    det, T = bool(g["deterministic"]), float(g["temperature"])
+    noise, tie, u = replay_draws(g)
+    B = g["obs"].shape[0]
+    eng = _engine(mzh, n, S, B, sup, flat)
+    tt = lambda a: None if a is None else torch.tensor(np.asarray(a), device=DEV)
+    o = eng.search(S, obs=tt(g["obs"].astype(np.float32)), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u),
+                   temperature=T, deterministic=det, discount=float(g["discount"]))
+    o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+    ref = oracle.search(n, S, g["obs"], flat=flat, support=sup, noise=noise, tie_idx=tie, action_u=u,
+                        temperature=T, deterministic=det, discount=float(g["discount"]))
+    assert np.array_equal(o["visits"], ref["visits"])
+    assert np.array_equal(o["root_q"], ref["rootQ"])
+    assert np.array_equal(o["pi"], ref["pi"]) and np.array_equal(o["action"], ref["action"])
+    assert np.array_equal(o["sel_steps"], ref["sel_steps"])
+    # and against the reference's own visit counts (torch-CPU network): report agreement
+    agree = (o["visits"] == g["visits"]).all(1).mean()
+    assert agree >= 0.5, agree
+
+
+@pytest.mark.parametrize("B,S,n", [(40, 50, 4), (700, 25, 3), (9000, 8, 4)])
+def test_search_batched_vs_oracle_random_roots(mzh, oracle, B, S, n):
+    """Ragged batches (not multiples of the 16/32-root tile), both tile sizes, vs the oracle."""
+    flat, in_dim, sup = _weights(oracle, f"weights_N{n}_s0")
+    rs = np.random.RandomState(B + S)
+    st = rs.randint(0, 3, (B, n))
+    obs = np.zeros((B, 3 * n), np.float32)
+    obs[np.arange(B)[:, None], np.arange(n) * 3 + st] = 1
+    from muzero_hanoi_amd import rng
+
+    noise, tie, u = rng.synthetic_draws(B, deterministic=False, alpha=0.25, seed=B)
+    eng = _engine(mzh, n, S, B, sup, flat)
+    tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
+    o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0)
+    o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+    nchk = min(B, 300)
+    ref = oracle.search(n, S, obs[:nchk], flat=flat, support=sup, noise=noise[:nchk], tie_idx=tie[:nchk],
+                        action_u=u[:nchk], temperature=1.0)
+    assert np.array_equal(o["visits"][:nchk], ref["visits"])
+    assert np.array_equal(o["root_q"][:nchk], ref["rootQ"])
+    assert np.array_equal(o["action"][:nchk], ref["action"])
+    assert np.all(o["visits"].sum(1) == S)
