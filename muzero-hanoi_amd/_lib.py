@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (must precede loading libmzh.so, see above)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmzh.so")
+LIB_PATH = os.environ.get("MZH_LIB") or os.path.join(HERE, "libmzh.so")  # MZH_LIB: diagnostic builds
 
 MZH_OK = 0
 MZH_ERR_ARG = -1

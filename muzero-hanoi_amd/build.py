@@ -29,16 +29,20 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose=False, force=False):
-    os.makedirs(OBJ, exist_ok=True)
+def build(verbose=False, force=False, diag=False):
+    """diag=True builds libmzh_diag.so with -DMZH_STAMPS (in-kernel phase stamps; never shipped)."""
+    obj_dir = OBJ + ("_diag" if diag else "")
+    lib_path = LIB.replace("libmzh.so", "libmzh_diag.so") if diag else LIB
+    flags = FLAGS + (["-DMZH_STAMPS"] if diag else [])
+    os.makedirs(obj_dir, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     headers.append(os.path.join(REPO, "include", "mzh.h"))
     jobs = []
     for src in SOURCES:
         s = os.path.join(CSRC, src)
-        o = os.path.join(OBJ, src.replace(".hip", ".o"))
+        o = os.path.join(obj_dir, src.replace(".hip", ".o"))
         if force or _stale(o, [s] + headers):
-            jobs.append([HIPCC, *FLAGS, "-c", s, "-o", o])
+            jobs.append([HIPCC, *flags, "-c", s, "-o", o])
 
     def run(cmd):
         if verbose:
@@ -52,12 +56,12 @@ def build(verbose=False, force=False):
         for err in ex.map(run, jobs):
             if verbose and err:
                 print(err, file=sys.stderr)
-    objs = [os.path.join(OBJ, s.replace(".hip", ".o")) for s in SOURCES]
-    if force or jobs or _stale(LIB, objs):
-        run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB,
+    objs = [os.path.join(obj_dir, s.replace(".hip", ".o")) for s in SOURCES]
+    if force or jobs or _stale(lib_path, objs):
+        run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", lib_path,
              "-Wl,-rpath,/opt/rocm/lib"])
-    return LIB
+    return lib_path
 
 
 if __name__ == "__main__":
-    print(build(verbose=True, force="--force" in sys.argv))
+    print(build(verbose=True, force="--force" in sys.argv, diag="--diag" in sys.argv))

@@ -1,6 +1,7 @@
 // mzh_api.hip -- C ABI (include/mzh.h) over the gfx950 kernels.  No exceptions cross the ABI;
 // every entry point returns a status and records a thread-local message.
 #include <math.h>
+#include <stdlib.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -270,7 +271,16 @@ extern "C" int mzh_hanoi_solver(int n_disks, int goal_peg, int B, const uint8_t*
 }
 
 // ---- inference ----
-static int pick_rows(int B) { return B >= 256 * 32 ? 32 : 16; }
+// roots (rows) per workgroup: 32 when that still gives >= 256 workgroups, else 16.
+// MZH_ROWS=16|32 in the environment forces a tile size (A/B experiments only).
+static int pick_rows(int B) {
+  static const int forced = [] {
+    const char* v = getenv("MZH_ROWS");
+    return v ? atoi(v) : 0;
+  }();
+  if (forced == 16 || forced == 32) return forced;
+  return B >= 256 * 32 ? 32 : 16;
+}
 
 extern "C" int mzh_initial_inference(mzh_engine* eng, int B, const float* obs, float* h, float* reward, float* pi,
                                      float* value, float* policy_logits, float* value_logits, mzh_stream stream) {

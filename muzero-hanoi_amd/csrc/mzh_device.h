@@ -21,6 +21,28 @@
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------------------------------
+// Diagnostic phase stamps (only in the -DMZH_STAMPS build, libmzh_diag.so; never in libmzh.so).
+// Lane 0 of every wave accumulates s_memtime deltas per phase into mzh_stamp_acc[wave][phase].
+// ------------------------------------------------------------------------------------------
+#define MZH_NSTAMP 24
+#ifdef MZH_STAMPS
+__device__ unsigned long long mzh_stamp_acc[8][MZH_NSTAMP];
+#define MZH_STAMP_DECL unsigned long long mzh_t_prev = __builtin_amdgcn_s_memtime();
+#define MZH_STAMP(ph)                                                                       \
+  do {                                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();                                   \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x == 0)                                         \
+      atomicAdd(&mzh_stamp_acc[threadIdx.x >> 6][ph], t_ - mzh_t_prev);                      \
+    mzh_t_prev = t_;                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+  } while (0)
+#else
+#define MZH_STAMP_DECL
+#define MZH_STAMP(ph) do {} while (0)
+#endif
+
+// ------------------------------------------------------------------------------------------
 // fp32 math (networks.py:152-196)
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ float mzh_expf(float x) {
@@ -222,77 +244,247 @@ __device__ __forceinline__ void mzh_run_jobs(const MzhJob* jobs, int KB, const f
   }
 }
 
-// normalize_h_state (networks.py:191-196): rows of `src` (stride 66) -> `dst`; one wave per row.
-template <int R>
-__device__ __forceinline__ void mzh_normalize_rows(const float* src, float* dst, int wave, int lane) {
-  for (int row = wave; row < R; row += MZH_THREADS / MZH_WAVE) {
-    float v = src[row * MZH_LD64 + lane];
-    float mn = v, mx = v;
+// ------------------------------------------------------------------------------------------
+// Pipelined chunks: a chunk is NJ output tiles (16 columns each) sharing one A operand,
+// K = 16*KB with NJ*KB <= 16, so a chunk's B fragments are exactly 16 float4 per lane.  Each wave
+// fetches the NEXT chunk's weights (and biases) while its MFMAs consume the current one; loads stay
+// in flight across __syncthreads (no LDS-DMA is outstanding, so the barrier does not drain them).
+// ------------------------------------------------------------------------------------------
+struct MzhChunk {
+  const float4* w[4];
+  const float* bias[4];  // already offset to the tile's first column
+  float* out;            // LDS output base
+  int col0[4];
+  int ldo, nj;           // nj: active tiles (wave-uniform), <= NJ
+};
+
+__device__ __forceinline__ MzhChunk mzh_chunk(const MzhLayer& L, int nt0, int nj, float* out, int ldo) {
+  MzhChunk c;
+  c.out = out;
+  c.ldo = ldo;
+  c.nj = nj;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      float a = __shfl_xor(mn, o);
-      float b = __shfl_xor(mx, o);
-      mn = a < mn ? a : mn;
-      mx = b > mx ? b : mx;
+  for (int q = 0; q < 4; ++q) {
+    const int nt = nt0 + (q < nj ? q : 0);
+    c.w[q] = L.w + (size_t)nt * L.kb * 64;
+    c.bias[q] = L.b + nt * 16;
+    c.col0[q] = nt * 16;
+  }
+  return c;
+}
+
+template <int NJ, int KB, bool ALL = false>
+__device__ __forceinline__ void mzh_fetch(floatx4* f, float* bv, const MzhChunk& c, int lane) {
+  static_assert(NJ * KB <= 16, "chunk too large");
+#pragma unroll
+  for (int q = 0; q < NJ; ++q) {
+    if (ALL || q < c.nj) {
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        const float4 t = c.w[q][kb * 64 + lane];
+        f[q * KB + kb] = floatx4{t.x, t.y, t.z, t.w};
+      }
+      bv[q] = c.bias[q][lane & 15];
     }
-    float d = (mx - mn) + 9.999999939225290290778502821922302246094e-09f;
-    dst[row * MZH_LD64 + lane] = (v - mn) / d;
   }
 }
 
-// Heads epilogue: value (wave 0), reward (wave 1, recurrent only), policy softmax (wave 2).
-template <int R>
-__device__ __forceinline__ void mzh_heads(MlpSmem<R>& sm, int support, bool recurrent, int wave, int lane) {
-  if (lane < R) {
-    const int row = lane;
-    if (wave == 0) {
-      sm.value[row] = mzh_logits_to_value(&sm.lval[row * MZH_LDSUP], support);
-    } else if (wave == 1) {
-      sm.reward[row] = recurrent ? mzh_logits_to_value(&sm.lrwd[row * MZH_LDSUP], support) : 0.0f;
-    } else if (wave == 2) {
-      float p[MZH_A];
-      mzh_softmax6(&sm.lpol[row * MZH_LDPOL], p);
+// acc = A[rows][0:16KB] . W-tiles ; epilogue (+onehot) + bias (+relu) -> LDS
+// ALL: every tile of the chunk is active (compile-time: no per-tile branches, so the epilogue of
+// one chunk can be scheduled against the MFMAs of the next)
+template <int MT, int NJ, int KB, bool ALL = false>
+__device__ __forceinline__ void mzh_mma_store(const floatx4* f, const float* bv, const MzhChunk& c, const float* A,
+                                              int lda, bool relu, const float* ohv, int lane) {
+  const int r = lane & 15, g = lane >> 4;
+  floatx4 acc[NJ][MT];
 #pragma unroll
-      for (int a = 0; a < MZH_A; ++a) sm.pi[row * 8 + a] = p[a];
+  for (int q = 0; q < NJ; ++q)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[q][m] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = kb * 16 + j * 4 + g;
+      float a[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) a[m] = A[(m * 16 + r) * lda + k];
+#pragma unroll
+      for (int q = 0; q < NJ; ++q) {
+        if (ALL || q < c.nj) {
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+            acc[q][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], f[q * KB + kb][j], acc[q][m], 0, 0, 0);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NJ; ++q) {
+    if (ALL || q < c.nj) {
+      const int col = c.col0[q] + r;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m * 16 + g * 4 + i;
+          float v = acc[q][m][i];
+          if (ohv) v = v + ohv[(q * MT + m) * 4 + i];  // one-hot action column (k = 64 + a)
+          v = v + bv[q];
+          if (relu) v = v > 0.0f ? v : 0.0f;
+          c.out[row * c.ldo + col] = v;
+        }
+      }
     }
   }
 }
 
-// prediction (networks.py:140-150) on sm.x (normalised latent): policy/value hidden + heads.
+// normalize_h_state (networks.py:191-196): 8 lanes per row, 8 elements per lane.
 template <int R>
-__device__ __forceinline__ void mzh_prediction_gemms(MlpSmem<R>& sm, const MzhNet& net, int wave, int lane) {
-  constexpr int MT = R / 16;
-  // pol0 + val0: 32 tiles, 8 per wave, two chunks of 4
+__device__ __forceinline__ void mzh_normalize_par(const float* src, float* dst, int tid) {
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int id0 = wave * 8 + c * 4;
-    const bool val = id0 >= 16;
-    const MzhLayer& L = val ? net.val0 : net.pol0;
-    MzhJob jobs[4];
+  for (int base = 0; base < R; base += MZH_THREADS / 8) {
+    const int row = base + (tid >> 3), part = tid & 7;
+    if (row < R) {
+      float v[8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      jobs[q] = mzh_job(sm.x, MZH_LD64, L, (id0 + q) & 15, val ? sm.hidV : sm.hidP, MZH_LD256, 1);
-    mzh_run_jobs<MT, 4>(jobs, L.kb, nullptr, nullptr, lane);
+      for (int i = 0; i < 8; ++i) v[i] = src[row * MZH_LD64 + part * 8 + i];
+      float mn = v[0], mx = v[0];
+#pragma unroll
+      for (int i = 1; i < 8; ++i) {
+        mn = v[i] < mn ? v[i] : mn;
+        mx = v[i] > mx ? v[i] : mx;
+      }
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) {
+        const float a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+      }
+      const float d = (mx - mn) + 9.999999939225290290778502821922302246094e-09f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dst[row * MZH_LD64 + part * 8 + i] = (v[i] - mn) / d;
+    }
   }
-  __syncthreads();
-  // pol2 (1 tile) + val2 (support 33: 3 tiles, support 1: 1 tile)
+}
+
+// Heads: value / reward transforms (networks.py:152-189) with 4 lanes per (row, head) for the
+// max and the 33 exps / divides; the two order-sensitive sums stay sequential in one lane (the
+// oracle's order) over register-staged values.  Then the policy softmax with 8 lanes per row.
+// `scratch` >= 2R*36 floats.
+template <int R>
+__device__ __forceinline__ void mzh_heads_par(MlpSmem<R>& sm, float* scratch, int support, bool recurrent, int tid) {
+  const int lane = tid & 63;
   {
-    int id = wave;
-    bool run = id < 1 + net.val2.nt;
-    if (run) {
-      MzhJob job = id == 0 ? mzh_job(sm.hidP, MZH_LD256, net.pol2, 0, sm.lpol, MZH_LDPOL, 0)
-                           : mzh_job(sm.hidV, MZH_LD256, net.val2, id - 1, sm.lval, MZH_LDSUP, 0);
-      mzh_run_jobs<MT, 1>(&job, net.pol2.kb, nullptr, nullptr, lane);
+    const int p = tid >> 2, q = tid & 3;
+    const bool active = p < 2 * R;
+    const bool isr = p >= R;
+    const int row = isr ? p - R : p;
+    const bool trans = active && support != 1 && !(isr && !recurrent);
+    const float* l = (isr ? sm.lrwd : sm.lval) + row * MZH_LDSUP;
+    float* ex = scratch + p * 36;
+    if (trans) {
+      float lv[9];
+      float m = -__builtin_inff();
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        const int k = q + 4 * i;
+        lv[i] = k < 33 ? l[k] : -__builtin_inff();
+        m = lv[i] > m ? lv[i] : m;
+      }
+      float t = __shfl_xor(m, 1);
+      m = t > m ? t : m;
+      t = __shfl_xor(m, 2);
+      m = t > m ? t : m;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        const int k = q + 4 * i;
+        if (k < 33) ex[k] = mzh_expf(lv[i] - m);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    float s = 0.0f;
+    if (trans && q == 0) {
+      float e[33];
+#pragma unroll
+      for (int k = 0; k < 33; ++k) e[k] = ex[k];
+#pragma unroll
+      for (int k = 0; k < 33; ++k) s = s + e[k];
+    }
+    s = __shfl(s, lane & ~3);
+    if (trans) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        const int k = q + 4 * i;
+        if (k < 33) ex[k] = ex[k] / s;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (active && q == 0) {
+      float result;
+      if (trans) {
+        float pk[33];
+#pragma unroll
+        for (int k = 0; k < 33; ++k) pk[k] = ex[k];
+        float x = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 33; ++k) {
+          const float prod = pk[k] * (float)(k - 16);
+          x = x + prod;
+        }
+        result = mzh_signed_parabolic(x);
+      } else {
+        result = (isr && !recurrent) ? 0.0f : l[0];
+      }
+      (isr ? sm.reward : sm.value)[row] = result;
     }
   }
-  __syncthreads();
+  {  // policy softmax (networks.py:83,109): 8 lanes per row, lanes 0..5 hold one logit each
+    const int row = tid >> 3, a = tid & 7;
+    if (row < R) {
+      const float lg = a < MZH_A ? sm.lpol[row * MZH_LDPOL + a] : -__builtin_inff();
+      float m = lg;
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) {
+        const float t = __shfl_xor(m, o);
+        m = t > m ? t : m;
+      }
+      const float e = a < MZH_A ? mzh_expf(lg - m) : 0.0f;
+      const int base = lane & ~7;
+      float ev[MZH_A];
+#pragma unroll
+      for (int i = 0; i < MZH_A; ++i) ev[i] = __shfl(e, base + i);
+      float s = 0.0f;
+#pragma unroll
+      for (int i = 0; i < MZH_A; ++i) s = s + ev[i];
+      if (a < MZH_A) sm.pi[row * 8 + a] = e / s;
+    }
+  }
+}
+
+// The per-wave chunk schedule of the prediction function (networks.py:140-150) on sm.x:
+//   C5/C6: pol0 (waves 0,1) or val0 (waves 2,3), 4 tiles each;  C7: pol2 (wave 0) / val2 (waves 1..)
+template <int R>
+__device__ __forceinline__ MzhChunk mzh_pred_chunk(MlpSmem<R>& sm, const MzhNet& net, int wave, int c) {
+  const int id0 = wave * 8 + c * 4;
+  return id0 >= 16 ? mzh_chunk(net.val0, id0 - 16, 4, sm.hidV, MZH_LD256)
+                   : mzh_chunk(net.pol0, id0, 4, sm.hidP, MZH_LD256);
+}
+template <int R>
+__device__ __forceinline__ MzhChunk mzh_head_chunk(MlpSmem<R>& sm, const MzhNet& net, int wave) {
+  if (wave == 0) return mzh_chunk(net.pol2, 0, 1, sm.lpol, MZH_LDPOL);
+  return mzh_chunk(net.val2, wave - 1 < net.val2.nt ? wave - 1 : 0, wave - 1 < net.val2.nt ? 1 : 0, sm.lval, MZH_LDSUP);
 }
 
 // initial_inference (networks.py:71-94): sm.x holds obs rows zero-padded to 16*rep0.kb.
 template <int R>
-__device__ void mzh_mlp_initial(MlpSmem<R>& sm, const MzhNet& net, int wave, int lane) {
+__device__ void mzh_mlp_initial(MlpSmem<R>& sm, const MzhNet& net, int wave_in, int lane) {
   constexpr int MT = R / 16;
-  {  // rep0: 16 tiles, 4 per wave
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(wave_in);
+  floatx4 fa[16], fb[16];
+  float ba[4], bb[4];
+  {  // rep0: 16 tiles, 4 per wave (K = 3N padded: runtime k-blocks)
     MzhJob jobs[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) jobs[q] = mzh_job(sm.x, MZH_LD64, net.rep0, wave * 4 + q, sm.hidP, MZH_LD256, 1);
@@ -303,46 +495,102 @@ __device__ void mzh_mlp_initial(MlpSmem<R>& sm, const MzhNet& net, int wave, int
     MzhJob job = mzh_job(sm.hidP, MZH_LD256, net.rep2, wave, sm.hraw, MZH_LD64, 0);
     mzh_run_jobs<MT, 1>(&job, net.rep2.kb, nullptr, nullptr, lane);
   }
+  const MzhChunk c5 = mzh_pred_chunk<R>(sm, net, wave, 0), c6 = mzh_pred_chunk<R>(sm, net, wave, 1);
+  const MzhChunk c7 = mzh_head_chunk<R>(sm, net, wave);
+  mzh_fetch<4, 4, true>(fa, ba, c5, lane);
+  mzh_fetch<4, 4, true>(fb, bb, c6, lane);
   __syncthreads();
-  mzh_normalize_rows<R>(sm.hraw, sm.x, wave, lane);
+  mzh_normalize_par<R>(sm.hraw, sm.x, tid);
   __syncthreads();
-  mzh_prediction_gemms<R>(sm, net, wave, lane);
-  mzh_heads<R>(sm, net.support, false, wave, lane);
+  mzh_mma_store<MT, 4, 4, true>(fa, ba, c5, sm.x, MZH_LD64, true, nullptr, lane);
+  mzh_fetch<1, 16>(fa, ba, c7, lane);
+  mzh_mma_store<MT, 4, 4, true>(fb, bb, c6, sm.x, MZH_LD64, true, nullptr, lane);
+  __syncthreads();
+  mzh_mma_store<MT, 1, 16>(fa, ba, c7, c7.out == sm.lpol ? sm.hidP : sm.hidV, MZH_LD256, false, nullptr, lane);
+  __syncthreads();
+  mzh_heads_par<R>(sm, sm.hidR, net.support, false, tid);
   __syncthreads();
 }
 
-// recurrent_inference (networks.py:96-138): sm.x holds parent latents, sm.act the actions.
-// Output: sm.x = normalised new latent, sm.pi / sm.value / sm.reward.
+// recurrent_inference (networks.py:96-138), split so the first two chunks' weights (dyn0, dyn2)
+// can be fetched early -- across the search kernel's tree phase -- into fa/fb:
+//   mzh_mlp_fetch12 : issue the loads of chunk 1 (dyn0) into fa and chunk 2 (dyn2) into fb
+//   mzh_mlp_recurrent_body<R, NEXT> : the MLP; with NEXT it re-issues fetch12 for the next step
+// Input: sm.x = parent latents, sm.act = actions.  Output: sm.x = normalised new latent,
+// sm.pi / sm.value / sm.reward.
+template <int R>
+__device__ __forceinline__ void mzh_mlp_fetch12(MlpSmem<R>& sm, const MzhNet& net, int wave_in, int lane, floatx4* fa,
+                                                float* ba, floatx4* fb, float* bb) {
+  const int wave = __builtin_amdgcn_readfirstlane(wave_in);
+  mzh_fetch<4, 4, true>(fa, ba, mzh_chunk(net.dyn0, wave * 4, 4, sm.hidP, MZH_LD256), lane);
+  mzh_fetch<1, 16, true>(fb, bb, mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64), lane);
+}
+
+template <int R, bool NEXT>
+__device__ __forceinline__ void mzh_mlp_recurrent_body(MlpSmem<R>& sm, const MzhNet& net, int wave_in, int lane,
+                                                       floatx4* fa, float* ba, floatx4* fb, float* bb) {
+  constexpr int MT = R / 16;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(wave_in);  // wave-uniform -> chunk descriptors in SGPRs
+  MZH_STAMP_DECL
+  {
+    // one-hot columns of the dynamics first layer for this lane's rows (k = 64 + action)
+    float oh[4 * MT * 4];
+    const int r = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          oh[(q * MT + m) * 4 + i] = net.dyn0_onehot[sm.act[m * 16 + g * 4 + i] * MZH_F + (wave * 4 + q) * 16 + r];
+    MZH_STAMP(0);
+    mzh_mma_store<MT, 4, 4, true>(fa, ba, mzh_chunk(net.dyn0, wave * 4, 4, sm.hidP, MZH_LD256), sm.x, MZH_LD64, true, oh,
+                            lane);  // dyn0 + one-hot + bias, relu
+  }
+  MZH_STAMP(1);
+  __syncthreads();
+  mzh_fetch<4, 4, true>(fa, ba, mzh_chunk(net.rwd0, wave * 4, 4, sm.hidR, MZH_LD256), lane);
+  MZH_STAMP(2);
+  mzh_mma_store<MT, 1, 16, true>(fb, bb, mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64), sm.hidP, MZH_LD256, false,
+                                 nullptr, lane);  // dyn2 -> h'
+  MZH_STAMP(3);
+  __syncthreads();
+  const bool has_r2 = wave < net.rwd2.nt;
+  mzh_fetch<1, 16>(fb, bb, mzh_chunk(net.rwd2, has_r2 ? wave : 0, has_r2 ? 1 : 0, sm.lrwd, MZH_LDSUP), lane);
+  MZH_STAMP(4);
+  mzh_normalize_par<R>(sm.hraw, sm.x, tid);
+  MZH_STAMP(5);
+  mzh_mma_store<MT, 4, 4, true>(fa, ba, mzh_chunk(net.rwd0, wave * 4, 4, sm.hidR, MZH_LD256), sm.hraw, MZH_LD64, true,
+                          nullptr, lane);  // rwd0 on h' (networks.py:132)
+  MZH_STAMP(6);
+  __syncthreads();
+  mzh_fetch<4, 4, true>(fa, ba, mzh_pred_chunk<R>(sm, net, wave, 0), lane);
+  MZH_STAMP(7);
+  mzh_mma_store<MT, 1, 16>(fb, bb, mzh_chunk(net.rwd2, has_r2 ? wave : 0, has_r2 ? 1 : 0, sm.lrwd, MZH_LDSUP),
+                           sm.hidR, MZH_LD256, false, nullptr, lane);  // rwd2 -> reward logits
+  mzh_fetch<4, 4, true>(fb, bb, mzh_pred_chunk<R>(sm, net, wave, 1), lane);
+  MZH_STAMP(8);
+  mzh_mma_store<MT, 4, 4, true>(fa, ba, mzh_pred_chunk<R>(sm, net, wave, 0), sm.x, MZH_LD64, true, nullptr, lane);
+  mzh_fetch<1, 16>(fa, ba, mzh_head_chunk<R>(sm, net, wave), lane);
+  mzh_mma_store<MT, 4, 4, true>(fb, bb, mzh_pred_chunk<R>(sm, net, wave, 1), sm.x, MZH_LD64, true, nullptr, lane);
+  MZH_STAMP(9);
+  __syncthreads();
+  mzh_mma_store<MT, 1, 16>(fa, ba, mzh_head_chunk<R>(sm, net, wave), wave == 0 ? sm.hidP : sm.hidV, MZH_LD256,
+                           false, nullptr, lane);  // pol2 / val2
+  if (NEXT) mzh_mlp_fetch12<R>(sm, net, wave, lane, fa, ba, fb, bb);  // next step's first chunks
+  MZH_STAMP(10);
+  __syncthreads();
+  mzh_heads_par<R>(sm, sm.hidR, net.support, true, tid);
+  MZH_STAMP(11);
+  __syncthreads();
+  MZH_STAMP(12);
+}
+
 template <int R>
 __device__ void mzh_mlp_recurrent(MlpSmem<R>& sm, const MzhNet& net, int wave, int lane) {
-  constexpr int MT = R / 16;
-  {  // dyn0 (h part, K=64) + one-hot column + bias, relu: 16 tiles, 4 per wave
-    MzhJob jobs[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) jobs[q] = mzh_job(sm.x, MZH_LD64, net.dyn0, wave * 4 + q, sm.hidP, MZH_LD256, 1);
-    mzh_run_jobs<MT, 4>(jobs, net.dyn0.kb, net.dyn0_onehot, sm.act, lane);
-  }
-  __syncthreads();
-  {  // dyn2: 4 tiles, 1 per wave -> un-normalised latent
-    MzhJob job = mzh_job(sm.hidP, MZH_LD256, net.dyn2, wave, sm.hraw, MZH_LD64, 0);
-    mzh_run_jobs<MT, 1>(&job, net.dyn2.kb, nullptr, nullptr, lane);
-  }
-  __syncthreads();
-  mzh_normalize_rows<R>(sm.hraw, sm.x, wave, lane);
-  {  // rwd0 on the UN-normalised latent (networks.py:132): 16 tiles, 4 per wave
-    MzhJob jobs[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) jobs[q] = mzh_job(sm.hraw, MZH_LD64, net.rwd0, wave * 4 + q, sm.hidR, MZH_LD256, 1);
-    mzh_run_jobs<MT, 4>(jobs, net.rwd0.kb, nullptr, nullptr, lane);
-  }
-  __syncthreads();
-  {  // rwd2 (support 33: 3 tiles / 1): waves 0..nt-1
-    if (wave < net.rwd2.nt) {
-      MzhJob job = mzh_job(sm.hidR, MZH_LD256, net.rwd2, wave, sm.lrwd, MZH_LDSUP, 0);
-      mzh_run_jobs<MT, 1>(&job, net.rwd2.kb, nullptr, nullptr, lane);
-    }
-  }
-  mzh_prediction_gemms<R>(sm, net, wave, lane);
-  mzh_heads<R>(sm, net.support, true, wave, lane);
-  __syncthreads();
+  floatx4 fa[16], fb[16];
+  float ba[4], bb[4];
+  mzh_mlp_fetch12<R>(sm, net, wave, lane, fa, ba, fb, bb);
+  mzh_mlp_recurrent_body<R, false>(sm, net, wave, lane, fa, ba, fb, bb);
 }

@@ -15,20 +15,43 @@
 // ------------------------------------------------------------------------------------------
 // tree block: the 6 children of one expanded node (+2 pad lanes)
 // ------------------------------------------------------------------------------------------
+struct MzhNX {
+  uint16_t N;  // child visit count (node.py:21)
+  int16_t X;   // expanded-node index of the child, -1 = not expanded (node.py:19 is_expanded)
+};
 struct __align__(16) MzhBlock {
-  uint16_t N[8];  // child visit counts (node.py:21)
-  int16_t X[8];   // expanded-node index of the child, -1 = leaf (node.py:19 is_expanded)
-  float R[8];     // child reward (python float of an fp32 value, node.py:25)
-  float P[8];     // child prior, fp32 (node.py:16)
-  double W[8];    // child summed value, fp64 (node.py:22)
+  MzhNX nx[8];  // N and X adjacent: one dword load per child in selection
+  float R[8];   // child reward (python float of an fp32 value, node.py:25)
+  float P[8];   // child prior, fp32 (node.py:16)
+  double W[8];  // child summed value, fp64 (node.py:22)
 };
 static_assert(sizeof(MzhBlock) == 160, "block layout");
 
+// the root's 6 children live in LDS for the whole search (every simulation starts there)
+struct MzhRootBlk {
+  double W[8];
+  double P64[8];  // prior as fp64: Dirichlet-mixed (np.float64) or the widened fp32 prior
+  float R[8];
+  int N[8];
+  int X[8];
+};
+
+// snapshot of the chosen child's statistics at each depth of the current simulation's path,
+// taken during selection so the backup needs no dependent global loads (depth < DC)
+struct MzhPathEnt {
+  double W;
+  float R;
+  int N;
+};
+
 template <int R>
 struct SearchSmem {
+  static constexpr int DC = R == 32 ? 16 : 32;
+  MzhRootBlk root[R];
+  MzhPathEnt pc[R][DC];
+  double bval[R][DC];  // value added at each cached path depth (backup value chain)
   double rootW[R];
   double mm[R][2];  // MinMaxStats (maximum, minimum)
-  double p64[R][8]; // root child priors as fp64 (Dirichlet-mixed or widened fp32)
   int rootN[R];
   int firstTie[R];
   int extra[R];
@@ -44,6 +67,47 @@ __device__ __forceinline__ double mzh_normalize(double v, double mx, double mn) 
   return v;
 }
 
+// ucb = fl32(Q) + fl32(U) for one child (node.py:90-123); `tnp` = table[N_parent]
+__device__ __forceinline__ float mzh_ucb(int Nc, double Wc, float Rc, double P64, bool p64_semantics, double tnp,
+                                         double disc, double mmax, double mmin) {
+  float q32 = 0.0f;
+  if (Nc > 0) q32 = (float)mzh_normalize((double)Rc + disc * (Wc / (double)Nc), mmax, mmin);
+  const double w = tnp / (double)(Nc + 1);
+  // np.float64 priors (Dirichlet-mixed root) or NumPy-1 promotion: fl32(fl64(prior * w));
+  // NumPy-2 with np.float32 priors: fl32(prior * fl32(w))
+  const float u32 = p64_semantics ? (float)(P64 * w) : (float)P64 * (float)w;
+  return q32 + u32;
+}
+
+// argmax over the 6 children held by the 8-lane group, with the reference's tie handling:
+// np.random.choice(argmax set) -- the first 6-way tie takes the host-drawn index, any other tie
+// is counted (RNG-stream divergence) and resolved to the lowest index.
+// max over each aligned group of 8 lanes with DPP (no LDS crossbar): quad_perm [1,0,3,2],
+// quad_perm [2,3,0,1], then row_half_mirror (lane i <-> 7-i inside the 8-lane half-row)
+__device__ __forceinline__ float mzh_max8(float v) {
+  float t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v = t > v ? t : v;
+  t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v = t > v ? t : v;
+  t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));
+  v = t > v ? t : v;
+  return v;
+}
+
+__device__ __forceinline__ int mzh_group_pick(float ucb, int c, int lane, int tie, int& firstTie, int& extra) {
+  const float m = mzh_max8(ucb);
+  const unsigned long long bal = __ballot(c < MZH_A && ucb == m);
+  const unsigned mask = (unsigned)(bal >> (lane & ~7)) & 0x3Fu;
+  const int cnt = __popc(mask);
+  if (cnt == 1) return __ffs(mask) - 1;
+  if (!firstTie && cnt == MZH_A) {
+    firstTie = 1;
+    return tie;
+  }
+  extra += 1;
+  return __ffs(mask) - 1;
+}
+
 // x ** e with numpy semantics for the exponents generate_play_policy can produce
 __device__ __forceinline__ double mzh_pow(double x, double e) {
   if (e == __builtin_rint(e) && e >= 1.0 && e <= 5.0) {
@@ -54,8 +118,12 @@ __device__ __forceinline__ double mzh_pow(double x, double e) {
   return pow(x, e);
 }
 
+// R = 32: one workgroup per CU (all 512 registers per lane); R = 16: two co-resident workgroups
+// per CU (<= 256 registers), so one workgroup's latency-bound tree phase overlaps the other's MFMAs.
 template <int R, bool REPLAY>
-__global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, MzhSearchParams p) {
+__global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kernel(MzhNet net, MzhSearchParams p) {
+  constexpr int DC = SearchSmem<R>::DC;
+  constexpr bool PF = R == 32;  // keep the next step's first weight chunks in flight across the tree phase
   extern __shared__ __align__(16) unsigned char smem_raw[];
   MlpSmem<R>& sm = *reinterpret_cast<MlpSmem<R>*>(smem_raw);
   SearchSmem<R>& st = *reinterpret_cast<SearchSmem<R>*>(smem_raw + sizeof(MlpSmem<R>));
@@ -78,6 +146,7 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
     st.firstTie[r] = 0;
     st.extra[r] = 0;
     st.steps[r] = 0;
+    st.depth[r] = 0;
     if (p.minmax_in && r < nvalid) {
       st.mm[r][0] = p.minmax_in[2 * (root0 + r)];
       st.mm[r][1] = p.minmax_in[2 * (root0 + r) + 1];
@@ -109,84 +178,88 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
   // root.expand(prior, h, 0) with optional Dirichlet mixing (mcts.py:57-69, 132-152)
   if (tid < R * 8) {
     const int r = tid >> 3, c = tid & 7;
-    if (r < nvalid) {
-      MzhBlock* b = reinterpret_cast<MzhBlock*>(p.tree) + (size_t)(root0 + r) * p.E;
-      const float pr = c < MZH_A ? sm.pi[r * 8 + c] : 0.0f;
-      b->N[c] = 0;
-      b->X[c] = -1;
-      b->R[c] = 0.0f;
-      b->P[c] = pr;
-      b->W[c] = 0.0;
-      if (c < MZH_A) {
-        double v = (double)pr;
-        if (noised) {
-          const float scaled = (float)(1.0 - p.eps) * pr;  // (1-eps) * prob, float32 array
-          v = (double)scaled + p.eps * p.noise[(size_t)(root0 + r) * MZH_A + c];
-        }
-        st.p64[r][c] = v;
-      }
+    MzhRootBlk& rb = st.root[r];
+    const float pr = (r < nvalid && c < MZH_A) ? sm.pi[r * 8 + c] : 0.0f;
+    rb.N[c] = 0;
+    rb.X[c] = -1;
+    rb.R[c] = 0.0f;
+    rb.W[c] = 0.0;
+    double v = (double)pr;
+    if (noised && r < nvalid && c < MZH_A) {
+      const float scaled = (float)(1.0 - p.eps) * pr;  // (1-eps) * prob, float32 array
+      v = (double)scaled + p.eps * p.noise[(size_t)(root0 + r) * MZH_A + c];
     }
+    rb.P64[c] = v;
   }
+  floatx4 fa[16], fb[16];
+  float ba[4], bb[4];
+  if (!REPLAY && PF) mzh_mlp_fetch12<R>(sm, net, wave, lane, fa, ba, fb, bb);
   __syncthreads();
 
+  MZH_STAMP_DECL
   for (int s = 0; s < S; ++s) {
+    MZH_STAMP(16);
     // ---------------- Phase 1: select (mcts.py:75-86; node.py:72-123) ----------------
     if (tid < R * 8) {
-      const int r = tid >> 3, c = tid & 7, gbase = lane & ~7;
+      const int r = tid >> 3, c = tid & 7;
       if (r < nvalid) {
         const MzhBlock* tb = reinterpret_cast<const MzhBlock*>(p.tree) + (size_t)(root0 + r) * p.E;
         const double mmax = st.mm[r][0], mmin = st.mm[r][1];
         int firstTie = st.firstTie[r];
         int extra = st.extra[r];
         const int tie = p.tie_idx ? p.tie_idx[root0 + r] : 0;
-        int e = 0, Np = st.rootN[r], depth = 0, pick = 0;
-        while (true) {
-          const MzhBlock* b = tb + e;
-          int Nc = 0, Xc = -1;
-          float ucb = -__builtin_inff();
-          if (c < MZH_A) {
-            Nc = b->N[c];
-            Xc = b->X[c];
-            const float Rc = b->R[c];
-            const float Pc = b->P[c];
-            const double Wc = b->W[c];
-            float q32 = 0.0f;
-            if (Nc > 0) q32 = (float)mzh_normalize((double)Rc + disc * (Wc / (double)Nc), mmax, mmin);
-            const double w = table[Np] / (double)(Nc + 1);
-            float u32;
-            if (e == 0 && noised)
-              u32 = (float)(st.p64[r][c] * w);
-            else if (p.np1)
-              u32 = (float)((double)Pc * w);
-            else
-              u32 = Pc * (float)w;
-            ucb = q32 + u32;
-          }
-          float m = ucb;
-#pragma unroll
-          for (int o = 1; o < 8; o <<= 1) {
-            const float t = __shfl_xor(m, o);
-            m = t > m ? t : m;
-          }
-          const unsigned long long bal = __ballot(c < MZH_A && ucb == m);
-          const unsigned mask = (unsigned)(bal >> gbase) & 0x3Fu;
-          const int cnt = __popc(mask);
-          if (cnt == 1) {
-            pick = __ffs(mask) - 1;
-          } else if (!firstTie && cnt == MZH_A) {
-            pick = tie;  // np.random.choice over the 6-way argmax set (host pre-drawn)
-            firstTie = 1;
-          } else {
-            pick = __ffs(mask) - 1;
-            extra += 1;
-          }
-          const int Nn = __shfl(Nc, gbase + pick);
-          const int Xn = __shfl(Xc, gbase + pick);
-          if (c == 0) path[r * PL + depth] = (uint16_t)(e * 8 + pick);
-          depth++;
-          if (Xn < 0) break;
+        // level 0: the root block (LDS)
+        int Nc = 0, Xc = -1;
+        double Wc = 0.0;
+        float Rc = 0.0f;
+        float ucb = -__builtin_inff();
+        if (c < MZH_A) {
+          const MzhRootBlk& rb = st.root[r];
+          Nc = rb.N[c];
+          Xc = rb.X[c];
+          Wc = rb.W[c];
+          Rc = rb.R[c];
+          ucb = mzh_ucb(Nc, Wc, Rc, rb.P64[c], noised || p.np1, table[st.rootN[r]], disc, mmax, mmin);
+        }
+        int pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
+        int gsrc = (lane & ~7) + pick;
+        int Nn = __shfl(Nc, gsrc), Xn = __shfl(Xc, gsrc);
+        double Wn = __shfl(Wc, gsrc);
+        float Rn = __shfl(Rc, gsrc);
+        if (c == 0) {
+          path[r * PL] = (uint16_t)pick;
+          st.pc[r][0] = MzhPathEnt{Wn, Rn, Nn};
+        }
+        int depth = 1, e = 0;
+        // deeper levels: tree blocks in HBM
+        while (Xn >= 0) {
           e = Xn;
-          Np = Nn;
+          const int Np = Nn;
+          const MzhBlock* b = tb + e;
+          ucb = -__builtin_inff();
+          Nc = 0;
+          Xc = -1;
+          Wc = 0.0;
+          Rc = 0.0f;
+          if (c < MZH_A) {
+            const uint32_t nx = *reinterpret_cast<const uint32_t*>(&b->nx[c]);
+            Nc = (int)(nx & 0xFFFFu);
+            Xc = (int)(int16_t)(nx >> 16);
+            Rc = b->R[c];
+            Wc = b->W[c];
+            ucb = mzh_ucb(Nc, Wc, Rc, (double)b->P[c], p.np1, table[Np], disc, mmax, mmin);
+          }
+          pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
+          gsrc = (lane & ~7) + pick;
+          Nn = __shfl(Nc, gsrc);
+          Xn = __shfl(Xc, gsrc);
+          Wn = __shfl(Wc, gsrc);
+          Rn = __shfl(Rc, gsrc);
+          if (c == 0) {
+            path[r * PL + depth] = (uint16_t)(e * 8 + pick);
+            if (depth < DC) st.pc[r][depth] = MzhPathEnt{Wn, Rn, Nn};
+          }
+          depth++;
         }
         if (c == 0) {
           st.depth[r] = depth;
@@ -198,7 +271,9 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
         }
       }
     }
+    MZH_STAMP(17);
     __syncthreads();
+    MZH_STAMP(18);
 
     // ---------------- Phase 2: expand via the network (mcts.py:88-106) ----------------
     if (!REPLAY) {
@@ -212,7 +287,13 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
       }
       if (tid < R) sm.act[tid] = tid < nvalid ? st.leafA[tid] : 0;
       __syncthreads();
-      mzh_mlp_recurrent<R>(sm, net, wave, lane);
+      MZH_STAMP(19);
+      if (PF) {
+        mzh_mlp_recurrent_body<R, PF>(sm, net, wave, lane, fa, ba, fb, bb);
+      } else {
+        mzh_mlp_recurrent<R>(sm, net, wave, lane);
+      }
+      MZH_STAMP(20);
       for (int i = tid; i < R * 16; i += MZH_THREADS) {
         const int r = i >> 4, qd = i & 15;
         if (r < nvalid) {
@@ -233,53 +314,97 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
       __syncthreads();
     }
 
+    MZH_STAMP(21);
     // ---------------- Phase 3: expand bookkeeping + backup (node.py:30-70) ----------------
+    // Lane 0 of each root's group runs the value chain leaf -> root (two fp64 ops per level, the
+    // only serial part); the 8 lanes then update the cached path nodes in parallel and reduce
+    // the MinMaxStats candidates (max/min are exact and order-free).
     if (tid < R * 8) {
       const int r = tid >> 3, c = tid & 7;
       if (r < nvalid) {
         MzhBlock* tb = reinterpret_cast<MzhBlock*>(p.tree) + (size_t)(root0 + r) * p.E;
+        MzhRootBlk& rb = st.root[r];
         const int enew = s + 1;
-        MzhBlock* nb = tb + enew;
-        nb->N[c] = 0;
-        nb->X[c] = -1;
+        MzhBlock* nb = tb + enew;  // the new expanded node's 6 children (node.py:44-49)
+        *reinterpret_cast<uint32_t*>(&nb->nx[c]) = 0xFFFF0000u;  // N = 0, X = -1
         nb->R[c] = 0.0f;
         nb->P[c] = c < MZH_A ? sm.pi[r * 8 + c] : 0.0f;
         nb->W[c] = 0.0;
+        const int le = st.leafE[r], la = st.leafA[r], depth = st.depth[r];
+        const float rew = sm.reward[r];
+        double lmax = -__builtin_inf(), lmin = __builtin_inf();
         if (c == 0) {
-          const int le = st.leafE[r], la = st.leafA[r];
-          const float rew = sm.reward[r];
-          tb[le].X[la] = (int16_t)enew;
-          tb[le].R[la] = rew;
-          double value = (double)sm.value[r];
-          double mmax = st.mm[r][0], mmin = st.mm[r][1];
-          const int depth = st.depth[r];
-          for (int j = depth - 1; j >= 0; --j) {
-            const int slot = path[r * PL + j];
-            MzhBlock* b = tb + (slot >> 3);
-            const int a = slot & 7;
-            const double rw = (j == depth - 1) ? (double)rew : (double)b->R[a];
-            const double W = b->W[a] + value;
-            const int N = b->N[a] + 1;
-            b->W[a] = W;
-            b->N[a] = (uint16_t)N;
-            const double q = rw + disc * (W / (double)N);
-            mmax = q > mmax ? q : mmax;
-            mmin = q < mmin ? q : mmin;
-            value = rw + disc * value;
+          if (le == 0) {
+            rb.X[la] = enew;
+            rb.R[la] = rew;
+          } else {
+            tb[le].nx[la].X = (int16_t)enew;
+            tb[le].R[la] = rew;
           }
-          const double W = st.rootW[r] + value;
+          double v = (double)sm.value[r];
+          for (int j = depth - 1; j >= 0; --j) {
+            double rw;
+            if (j < DC) {
+              st.bval[r][j] = v;
+              rw = (j == depth - 1) ? (double)rew : (double)st.pc[r][j].R;
+            } else {  // beyond the LDS path cache: update here from HBM
+              const int slot = path[r * PL + j];
+              const int e = slot >> 3, a = slot & 7;
+              rw = (j == depth - 1) ? (double)rew : (double)tb[e].R[a];
+              const double W = tb[e].W[a] + v;
+              const int N = tb[e].nx[a].N + 1;
+              tb[e].W[a] = W;
+              tb[e].nx[a].N = (uint16_t)N;
+              const double q = rw + disc * (W / (double)N);
+              lmax = q > lmax ? q : lmax;
+              lmin = q < lmin ? q : lmin;
+            }
+            v = rw + disc * v;
+          }
+          const double W = st.rootW[r] + v;
           const int N = st.rootN[r] + 1;
           st.rootW[r] = W;
           st.rootN[r] = N;
           const double q = 0.0 + disc * (W / (double)N);  // root rwd = 0.0
-          mmax = q > mmax ? q : mmax;
-          mmin = q < mmin ? q : mmin;
-          st.mm[r][0] = mmax;
-          st.mm[r][1] = mmin;
+          lmax = q > lmax ? q : lmax;
+          lmin = q < lmin ? q : lmin;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int jmax = depth < DC ? depth : DC;
+        for (int j = c; j < jmax; j += 8) {
+          const int slot = path[r * PL + j];
+          const int e = slot >> 3, a = slot & 7;
+          const MzhPathEnt pe = st.pc[r][j];
+          const double rw = (j == depth - 1) ? (double)rew : (double)pe.R;
+          const double W = pe.W + st.bval[r][j];
+          const int N = pe.N + 1;
+          if (e == 0) {
+            rb.W[a] = W;
+            rb.N[a] = N;
+          } else {
+            tb[e].W[a] = W;
+            tb[e].nx[a].N = (uint16_t)N;
+          }
+          const double q = rw + disc * (W / (double)N);
+          lmax = q > lmax ? q : lmax;
+          lmin = q < lmin ? q : lmin;
+        }
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+          const double tx = __shfl_xor(lmax, o), tn = __shfl_xor(lmin, o);
+          lmax = tx > lmax ? tx : lmax;
+          lmin = tn < lmin ? tn : lmin;
+        }
+        if (c == 0) {
+          const double mx = st.mm[r][0], mn = st.mm[r][1];
+          st.mm[r][0] = lmax > mx ? lmax : mx;
+          st.mm[r][1] = lmin < mn ? lmin : mn;
         }
       }
     }
+    MZH_STAMP(22);
     __syncthreads();
+    MZH_STAMP(23);
   }
 
   // ---------------- results (mcts.py:111-126, 154-176) ----------------
@@ -287,10 +412,9 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
     const int r = tid >> 3, c = tid & 7;
     if (r < nvalid && c == 0) {
       const int root = root0 + r;
-      const MzhBlock* b0 = reinterpret_cast<const MzhBlock*>(p.tree) + (size_t)root * p.E;
       int vis[MZH_A];
       for (int a = 0; a < MZH_A; ++a) {
-        vis[a] = b0->N[a];
+        vis[a] = st.root[r].N[a];
         p.visits[(size_t)root * MZH_A + a] = vis[a];
       }
       if (p.root_q) p.root_q[root] = st.rootN[r] == 0 ? 0.0 : st.rootW[r] / (double)st.rootN[r];
@@ -427,6 +551,16 @@ static hipError_t launch_infer_t(bool recurrent, const MzhNet& net, const MzhInf
     hipLaunchKernelGGL((mzh_initial_kernel<R>), dim3(grid), dim3(MZH_THREADS), smem, stream, net, p);
   return hipGetLastError();
 }
+
+#ifdef MZH_STAMPS
+// diagnostic build only: read and clear the accumulated phase stamps [8 waves][MZH_NSTAMP]
+extern "C" int mzh_diag_stamps(unsigned long long* host) {
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(mzh_stamp_acc), sizeof(mzh_stamp_acc)) != hipSuccess) return -2;
+  static unsigned long long zero[8][MZH_NSTAMP] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(mzh_stamp_acc), zero, sizeof(zero)) != hipSuccess) return -2;
+  return 0;
+}
+#endif
 
 hipError_t mzh_launch_infer(int R, bool recurrent, const MzhNet& net, const MzhInferParams& p, hipStream_t stream) {
   return R == 32 ? launch_infer_t<32>(recurrent, net, p, stream) : launch_infer_t<16>(recurrent, net, p, stream);
