@@ -78,6 +78,41 @@ __device__ __forceinline__ float mzh_signed_parabolic(float x) {
   return sg * (z * z - 1.0f);
 }
 
+// ------------------------------------------------------------------------------------------
+// 8-lane DPP reductions (aligned groups of 8 lanes; no LDS crossbar).  Steps: quad_perm
+// [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror (lane i <-> 7-i).  Every lane of the group ends
+// with the same bits: IEEE add/max are commutative, so the sum is exactly
+// ((s0+s1)+(s2+s3)) + ((s4+s5)+(s6+s7)) on every lane -- the order oracle/mzh_oracle.c uses.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float mzh_dpp_f(float v, int ctrl_sel) {
+  switch (ctrl_sel) {
+    case 0: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+    case 1: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+    default: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));
+  }
+}
+__device__ __forceinline__ float mzh_max8(float v) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float t = mzh_dpp_f(v, i);
+    v = t > v ? t : v;
+  }
+  return v;
+}
+__device__ __forceinline__ float mzh_min8(float v) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float t = mzh_dpp_f(v, i);
+    v = t < v ? t : v;
+  }
+  return v;
+}
+__device__ __forceinline__ float mzh_sum8(float v) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) v = v + mzh_dpp_f(v, i);
+  return v;
+}
+
 // logits_to_transformed_expected_value (networks.py:152-184); logits in LDS
 __device__ inline float mzh_logits_to_value(const float* l, int support) {
   if (support == 1) return l[0];
@@ -355,12 +390,8 @@ __device__ __forceinline__ void mzh_normalize_par(const float* src, float* dst, 
         mn = v[i] < mn ? v[i] : mn;
         mx = v[i] > mx ? v[i] : mx;
       }
-#pragma unroll
-      for (int o = 1; o < 8; o <<= 1) {
-        const float a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
-        mn = a < mn ? a : mn;
-        mx = b > mx ? b : mx;
-      }
+      mn = mzh_min8(mn);
+      mx = mzh_max8(mx);
       const float d = (mx - mn) + 9.999999939225290290778502821922302246094e-09f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) dst[row * MZH_LD64 + part * 8 + i] = (v[i] - mn) / d;
@@ -368,96 +399,77 @@ __device__ __forceinline__ void mzh_normalize_par(const float* src, float* dst, 
   }
 }
 
-// Heads: value / reward transforms (networks.py:152-189) with 4 lanes per (row, head) for the
-// max and the 33 exps / divides; the two order-sensitive sums stay sequential in one lane (the
-// oracle's order) over register-staged values.  Then the policy softmax with 8 lanes per row.
-// `scratch` >= 2R*36 floats.
+// Heads (networks.py:83,109,152-189): 8 lanes per (row, head).  Lane q owns logits k = q + 8i;
+// max / exp / divide are lane-parallel, and both 33-term sums use the fixed order of sum8_tree
+// in the oracle: sequential per-lane partials combined by the DPP tree (mzh_sum8).
 template <int R>
-__device__ __forceinline__ void mzh_heads_par(MlpSmem<R>& sm, float* scratch, int support, bool recurrent, int tid) {
-  const int lane = tid & 63;
-  {
-    const int p = tid >> 2, q = tid & 3;
-    const bool active = p < 2 * R;
-    const bool isr = p >= R;
-    const int row = isr ? p - R : p;
-    const bool trans = active && support != 1 && !(isr && !recurrent);
-    const float* l = (isr ? sm.lrwd : sm.lval) + row * MZH_LDSUP;
-    float* ex = scratch + p * 36;
-    if (trans) {
-      float lv[9];
-      float m = -__builtin_inff();
+__device__ __forceinline__ void mzh_value_head8(const float* l, int q, float* out) {
+  float e[5];
+  float m = -__builtin_inff();
 #pragma unroll
-      for (int i = 0; i < 9; ++i) {
-        const int k = q + 4 * i;
-        lv[i] = k < 33 ? l[k] : -__builtin_inff();
-        m = lv[i] > m ? lv[i] : m;
-      }
-      float t = __shfl_xor(m, 1);
-      m = t > m ? t : m;
-      t = __shfl_xor(m, 2);
-      m = t > m ? t : m;
+  for (int i = 0; i < 5; ++i) {
+    const int k = q + 8 * i;
+    e[i] = k < 33 ? l[k] : -__builtin_inff();
+    m = e[i] > m ? e[i] : m;
+  }
+  m = mzh_max8(m);
 #pragma unroll
-      for (int i = 0; i < 9; ++i) {
-        const int k = q + 4 * i;
-        if (k < 33) ex[k] = mzh_expf(lv[i] - m);
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    float s = 0.0f;
-    if (trans && q == 0) {
-      float e[33];
+  for (int i = 0; i < 5; ++i) e[i] = (q + 8 * i < 33) ? mzh_expf(e[i] - m) : 0.0f;
+  float a = e[0];
 #pragma unroll
-      for (int k = 0; k < 33; ++k) e[k] = ex[k];
+  for (int i = 1; i < 4; ++i) a = a + e[i];
+  if (q == 0) a = a + e[4];
+  const float s = mzh_sum8(a);
+  float x = 0.0f;
 #pragma unroll
-      for (int k = 0; k < 33; ++k) s = s + e[k];
-    }
-    s = __shfl(s, lane & ~3);
-    if (trans) {
-#pragma unroll
-      for (int i = 0; i < 9; ++i) {
-        const int k = q + 4 * i;
-        if (k < 33) ex[k] = ex[k] / s;
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (active && q == 0) {
-      float result;
-      if (trans) {
-        float pk[33];
-#pragma unroll
-        for (int k = 0; k < 33; ++k) pk[k] = ex[k];
-        float x = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 33; ++k) {
-          const float prod = pk[k] * (float)(k - 16);
-          x = x + prod;
-        }
-        result = mzh_signed_parabolic(x);
-      } else {
-        result = (isr && !recurrent) ? 0.0f : l[0];
-      }
-      (isr ? sm.reward : sm.value)[row] = result;
+  for (int i = 0; i < 5; ++i) {
+    const int k = q + 8 * i;
+    if (k < 33) {
+      const float pk = e[i] / s;
+      const float prod = pk * (float)(k - 16);
+      x = i == 0 ? prod : x + prod;
     }
   }
-  {  // policy softmax (networks.py:83,109): 8 lanes per row, lanes 0..5 hold one logit each
-    const int row = tid >> 3, a = tid & 7;
-    if (row < R) {
-      const float lg = a < MZH_A ? sm.lpol[row * MZH_LDPOL + a] : -__builtin_inff();
-      float m = lg;
+  x = mzh_sum8(x);
+  if (q == 0) *out = mzh_signed_parabolic(x);
+}
+
+template <int R>
+__device__ __forceinline__ void mzh_heads_par(MlpSmem<R>& sm, float* scratch, int support, bool recurrent, int tid) {
+  (void)scratch;
+  const int g = tid >> 3, q = tid & 7;  // 32 groups of 8 lanes over 256 threads
+  // value heads, then reward heads (recurrent), 32 rows per pass
 #pragma unroll
-      for (int o = 1; o < 8; o <<= 1) {
-        const float t = __shfl_xor(m, o);
-        m = t > m ? t : m;
+  for (int pass = 0; pass < 2; ++pass) {
+    const bool isr = pass == 1;
+    if (isr && !recurrent) {
+      if (tid < R) sm.reward[tid] = 0.0f;
+      continue;
+    }
+#pragma unroll
+    for (int row0 = 0; row0 < R; row0 += 32) {
+      const int row = row0 + g;
+      if (row < R) {
+        const float* l = (isr ? sm.lrwd : sm.lval) + row * MZH_LDSUP;
+        float* out = isr ? &sm.reward[row] : &sm.value[row];
+        if (support == 1) {
+          if (q == 0) *out = l[0];
+        } else {
+          mzh_value_head8<R>(l, q, out);
+        }
       }
-      const float e = a < MZH_A ? mzh_expf(lg - m) : 0.0f;
-      const int base = lane & ~7;
-      float ev[MZH_A];
+    }
+  }
+  // policy softmax: 8 lanes per row, lanes 0..5 hold one logit each
 #pragma unroll
-      for (int i = 0; i < MZH_A; ++i) ev[i] = __shfl(e, base + i);
-      float s = 0.0f;
-#pragma unroll
-      for (int i = 0; i < MZH_A; ++i) s = s + ev[i];
-      if (a < MZH_A) sm.pi[row * 8 + a] = e / s;
+  for (int row0 = 0; row0 < R; row0 += 32) {
+    const int row = row0 + g;
+    if (row < R) {
+      const float lg = q < MZH_A ? sm.lpol[row * MZH_LDPOL + q] : -__builtin_inff();
+      const float m = mzh_max8(lg);
+      const float e = q < MZH_A ? mzh_expf(lg - m) : 0.0f;
+      const float s = mzh_sum8(e);
+      if (q < MZH_A) sm.pi[row * 8 + q] = e / s;
     }
   }
 }

@@ -82,18 +82,6 @@ __device__ __forceinline__ float mzh_ucb(int Nc, double Wc, float Rc, double P64
 // argmax over the 6 children held by the 8-lane group, with the reference's tie handling:
 // np.random.choice(argmax set) -- the first 6-way tie takes the host-drawn index, any other tie
 // is counted (RNG-stream divergence) and resolved to the lowest index.
-// max over each aligned group of 8 lanes with DPP (no LDS crossbar): quad_perm [1,0,3,2],
-// quad_perm [2,3,0,1], then row_half_mirror (lane i <-> 7-i inside the 8-lane half-row)
-__device__ __forceinline__ float mzh_max8(float v) {
-  float t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
-  v = t > v ? t : v;
-  t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
-  v = t > v ? t : v;
-  t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));
-  v = t > v ? t : v;
-  return v;
-}
-
 __device__ __forceinline__ int mzh_group_pick(float ucb, int c, int lane, int tie, int& firstTie, int& extra) {
   const float m = mzh_max8(ucb);
   const unsigned long long bal = __ballot(c < MZH_A && ucb == m);
@@ -222,43 +210,37 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
           ucb = mzh_ucb(Nc, Wc, Rc, rb.P64[c], noised || p.np1, table[st.rootN[r]], disc, mmax, mmin);
         }
         int pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
-        int gsrc = (lane & ~7) + pick;
-        int Nn = __shfl(Nc, gsrc), Xn = __shfl(Xc, gsrc);
-        double Wn = __shfl(Wc, gsrc);
-        float Rn = __shfl(Rc, gsrc);
-        if (c == 0) {
+        // the picking lane records the path entry and its own statistics; one shuffle of the
+        // packed (N | X << 16) word moves the selection on
+        if (c == pick) {
           path[r * PL] = (uint16_t)pick;
-          st.pc[r][0] = MzhPathEnt{Wn, Rn, Nn};
+          st.pc[r][0] = MzhPathEnt{Wc, Rc, Nc};
         }
+        int nx = __shfl((Nc & 0xFFFF) | (Xc << 16), (lane & ~7) + pick);
         int depth = 1, e = 0;
         // deeper levels: tree blocks in HBM
-        while (Xn >= 0) {
-          e = Xn;
-          const int Np = Nn;
+        while ((nx >> 16) >= 0) {
+          e = nx >> 16;
+          const int Np = nx & 0xFFFF;
           const MzhBlock* b = tb + e;
           ucb = -__builtin_inff();
+          int nxc = (int)0xFFFF0000;
           Nc = 0;
-          Xc = -1;
           Wc = 0.0;
           Rc = 0.0f;
           if (c < MZH_A) {
-            const uint32_t nx = *reinterpret_cast<const uint32_t*>(&b->nx[c]);
-            Nc = (int)(nx & 0xFFFFu);
-            Xc = (int)(int16_t)(nx >> 16);
+            nxc = *reinterpret_cast<const int*>(&b->nx[c]);
+            Nc = nxc & 0xFFFF;
             Rc = b->R[c];
             Wc = b->W[c];
             ucb = mzh_ucb(Nc, Wc, Rc, (double)b->P[c], p.np1, table[Np], disc, mmax, mmin);
           }
           pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
-          gsrc = (lane & ~7) + pick;
-          Nn = __shfl(Nc, gsrc);
-          Xn = __shfl(Xc, gsrc);
-          Wn = __shfl(Wc, gsrc);
-          Rn = __shfl(Rc, gsrc);
-          if (c == 0) {
+          if (c == pick) {
             path[r * PL + depth] = (uint16_t)(e * 8 + pick);
-            if (depth < DC) st.pc[r][depth] = MzhPathEnt{Wn, Rn, Nn};
+            if (depth < DC) st.pc[r][depth] = MzhPathEnt{Wc, Rc, Nc};
           }
+          nx = __shfl(nxc, (lane & ~7) + pick);
           depth++;
         }
         if (c == 0) {
@@ -342,24 +324,29 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
             tb[le].R[la] = rew;
           }
           double v = (double)sm.value[r];
-          for (int j = depth - 1; j >= 0; --j) {
-            double rw;
-            if (j < DC) {
-              st.bval[r][j] = v;
-              rw = (j == depth - 1) ? (double)rew : (double)st.pc[r][j].R;
-            } else {  // beyond the LDS path cache: update here from HBM
-              const int slot = path[r * PL + j];
-              const int e = slot >> 3, a = slot & 7;
-              rw = (j == depth - 1) ? (double)rew : (double)tb[e].R[a];
-              const double W = tb[e].W[a] + v;
-              const int N = tb[e].nx[a].N + 1;
-              tb[e].W[a] = W;
-              tb[e].nx[a].N = (uint16_t)N;
-              const double q = rw + disc * (W / (double)N);
-              lmax = q > lmax ? q : lmax;
-              lmin = q < lmin ? q : lmin;
-            }
+          int j = depth - 1;
+          for (; j >= DC; --j) {  // beyond the LDS path cache (rare): update here from HBM
+            const int slot = path[r * PL + j];
+            const int e = slot >> 3, a = slot & 7;
+            const double rw = (j == depth - 1) ? (double)rew : (double)tb[e].R[a];
+            const double W = tb[e].W[a] + v;
+            const int N = tb[e].nx[a].N + 1;
+            tb[e].W[a] = W;
+            tb[e].nx[a].N = (uint16_t)N;
+            const double q = rw + disc * (W / (double)N);
+            lmax = q > lmax ? q : lmax;
+            lmin = q < lmin ? q : lmin;
             v = rw + disc * v;
+          }
+          if (j == depth - 1 && j >= 0) {  // the leaf (its reward was just set)
+            st.bval[r][j] = v;
+            v = (double)rew + disc * v;
+            --j;
+          }
+#pragma unroll 4
+          for (; j >= 0; --j) {
+            st.bval[r][j] = v;
+            v = (double)st.pc[r][j].R + disc * v;
           }
           const double W = st.rootW[r] + v;
           const int N = st.rootN[r] + 1;

@@ -133,16 +133,32 @@ float orc_expf(float x) {
   return p * s.f;
 }
 
+/* Fixed summation order shared with the device (8 lanes, one partial sum each):
+ *   s_q = v[q] + v[q+8] + v[q+16] + ...  (sequential, q = 0..7; 0 when q >= n)
+ *   sum = ((s_0 + s_1) + (s_2 + s_3)) + ((s_4 + s_5) + (s_6 + s_7))
+ * torch's own reduction order for these sums is an implementation detail of its vectorised
+ * kernels; any fixed order is an equally faithful restatement (within the tolerances of
+ * SURVEY.md 8a-10), and this one maps onto an 8-lane DPP tree. */
+static float sum8_tree(const float* v, int n) {
+  float s[8];
+  for (int q = 0; q < 8; ++q) {
+    float a = 0.0f;
+    if (q < n) {
+      a = v[q];
+      for (int k = q + 8; k < n; k += 8) a = a + v[k];
+    }
+    s[q] = a;
+  }
+  return ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+}
+
 /* F.softmax over the last dim (networks.py:83,109,170) */
 static void softmax(const float* l, int n, float* p) {
   float m = l[0];
   for (int i = 1; i < n; ++i)
     if (l[i] > m) m = l[i];
-  float s = 0.0f;
-  for (int i = 0; i < n; ++i) {
-    p[i] = orc_expf(l[i] - m);
-    s = s + p[i];
-  }
+  for (int i = 0; i < n; ++i) p[i] = orc_expf(l[i] - m);
+  const float s = sum8_tree(p, n);
   for (int i = 0; i < n; ++i) p[i] = p[i] / s;
 }
 
@@ -168,12 +184,9 @@ float orc_logits_to_value(const float* logits, int support) {
   float p[ORC_MAXSUP];
   softmax(logits, support, p);
   int half = (support - 1) / 2;
-  float x = 0.0f;
-  for (int k = 0; k < support; ++k) {
-    float prod = p[k] * (float)(k - half);
-    x = x + prod;
-  }
-  return orc_signed_parabolic(x);
+  float prod[ORC_MAXSUP];
+  for (int k = 0; k < support; ++k) prod[k] = p[k] * (float)(k - half);
+  return orc_signed_parabolic(sum8_tree(prod, support));
 }
 
 /* normalize_h_state (networks.py:191-196) */
