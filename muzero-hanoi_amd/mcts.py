@@ -18,6 +18,19 @@ from . import rng as _rng
 from .networks import engine_for
 
 
+_REPLAY_ENGINES = {}
+
+
+def _replay_engine(n_disks, n_sims):
+    from .engine import Engine
+
+    eng = _REPLAY_ENGINES.get(n_disks)
+    if eng is None or eng.max_sims < n_sims:
+        eng = Engine(n_disks, max(n_sims, 64), 1, 33)
+        _REPLAY_ENGINES[n_disks] = eng
+    return eng
+
+
 class MinMaxStats(object):
     """utils_mcts.py:1-16 (host mirror; the device carries the same two doubles)."""
 
@@ -33,6 +46,24 @@ class MinMaxStats(object):
         if self.maximum > self.minimum:
             return (value - self.minimum) / (self.maximum - self.minimum)
         return value
+
+
+class RecordedNetwork:
+    """Network duck type whose outputs were recorded (tree-only mode, mzh_search_replay).
+
+    calls: list of dicts, one per run_mcts call, each with root_pi [6] and, per simulation,
+    pi [S,6], reward [S], value [S] (fp32 values, exactly what the network returned)."""
+
+    def __init__(self, calls, n_disks, num_actions=6):
+        self.calls = list(calls)
+        self.n_disks = n_disks
+        self.num_actions = num_actions
+        self.cursor = 0
+
+    def next_call(self):
+        c = self.calls[self.cursor]
+        self.cursor += 1
+        return c
 
 
 class MCTS:
@@ -61,13 +92,20 @@ class MCTS:
                                      eps=self.root_exploration_eps)
         if not 0.0 <= temperature <= 1.0:  # raised after the search's draws, like mcts.py:163-166
             raise ValueError(f"Expect `temperature` to be in the range [0.0, 1.0], got {temperature}")
-        eng = engine_for(network, S, 1)
+        replay = None
+        if isinstance(network, RecordedNetwork):
+            eng = _replay_engine(network.n_disks, S)
+            call = network.next_call()
+            replay = {k: torch.as_tensor(np.asarray(call[k], np.float32)).to(eng.device)[None]
+                      for k in ("root_pi", "pi", "reward", "value")}
+        else:
+            eng = engine_for(network, S, 1)
         dev = eng.device
         obs = torch.as_tensor(np.asarray(state)).to(dev, torch.float32).reshape(1, -1)
         mm = torch.tensor([[self.min_max_stats.maximum, self.min_max_stats.minimum]], dtype=torch.float64, device=dev)
         t = lambda a: None if a is None else torch.from_numpy(np.asarray(a)).to(dev)
-        out = eng.search(S, obs=obs, tie_idx=t(tie), noise=t(noise), action_u=t(u), minmax_in=mm,
-                         temperature=float(temperature), deterministic=bool(deterministic),
+        out = eng.search(S, obs=None if replay else obs, replay=replay, tie_idx=t(tie), noise=t(noise), action_u=t(u),
+                         minmax_in=mm, temperature=float(temperature), deterministic=bool(deterministic),
                          discount=float(self.discount), eps=float(self.root_exploration_eps), np1_ucb=self.np1_ucb)
         host = {k: v.cpu().numpy() for k, v in out.items() if k != "_keep"}
         self.min_max_stats.maximum = float(host["minmax"][0, 0])

@@ -324,7 +324,60 @@ REPLAY_CASES = [
 ]
 
 
+def gen_episode(name, n, s, max_steps, seed, episode, deterministic, wseed=0, td=True, n_td=10):
+    """A whole Muzero._play_game episode (Muzero.py:153-207) of the reference, with every network
+    call recorded per search, so the self-play driver can be replayed bit-exactly."""
+    from Muzero import Muzero
+
+    env = TowersOfHanoi(N=n, max_steps=max_steps)
+    torch.manual_seed(wseed)
+    np.random.seed(seed)
+    mz = Muzero(env=env, s_space_size=3 * n, n_action=6, discount=0.8, dirichlet_alpha=0.25,
+                n_mcts_simulations=s, unroll_n_steps=5, batch_s=256, TD_return=td, n_TD_step=n_td,
+                lr=0.002, buffer_size=1000, priority_replay=True, device="cpu")
+    torch.manual_seed(wseed)
+    net = MuZeroNet(rpr_input_s=3 * n, action_s=6, lr=0.002, device="cpu", TD_return=td)
+    rec = Recorder(net)
+    mz.networks = rec
+    mz.mcts = TracingMCTS(discount=0.8, root_dirichlet_alpha=0.25, n_simulations=s, batch_s=256, device="cpu")
+    visits, mm = [], []
+    orig = mz.mcts.run_mcts
+
+    def run(*a, **k):
+        out = orig(*a, **k)
+        visits.append(mz.mcts.last_visits.astype(np.int32))
+        mm.append((mz.mcts.min_max_stats.maximum, mz.mcts.min_max_stats.minimum))
+        return out
+
+    mz.mcts.run_mcts = run
+    steps, states, rwds, actions, pi_probs, returns, priorities = mz._play_game(episode=episode,
+                                                                                deterministic=deterministic)
+    calls = rec.calls
+    assert len(calls) == steps * (s + 1)
+    out_pi = np.array([c[3][2] for c in calls], np.float32).reshape(steps, s + 1, 6)
+    out_rwd = np.array([c[3][1] for c in calls], np.float64).reshape(steps, s + 1)
+    out_v = np.array([c[3][3] for c in calls], np.float64).reshape(steps, s + 1)
+    obs = np.array([c[1] for c in calls[:: s + 1]], np.float64)
+    np.savez_compressed(
+        os.path.join(HERE, f"episode_{name}.npz"), n=n, s=s, max_steps=max_steps, seed=seed, episode=episode,
+        deterministic=int(deterministic), td=int(td), n_td=n_td, init_state_idx=env.init_state_idx,
+        steps=steps, obs=obs, out_pi=out_pi, out_rwd=out_rwd, out_v=out_v, visits=np.array(visits),
+        mm=np.array(mm, np.float64), states=states, rwds=rwds, actions=actions, pi_probs=pi_probs,
+        returns=returns, priorities=np.asarray(priorities, np.float32),
+        post_rng=np.random.random_sample(4),  # pins the RNG position after the episode
+    )
+
+
+EPISODE_CASES = [
+    ("n3s25_t1", 3, 25, 40, 3, 1, False),
+    ("n3s25_t05", 3, 25, 30, 5, 600, False),
+    ("n3s10_det", 3, 10, 25, 7, 900, True),
+]
+
+
 def main():
+    for name, n, s, ms, seed, ep, det in EPISODE_CASES:
+        gen_episode(name, n, s, ms, seed, ep, det)
     for n in (3, 4, 7):
         gen_env(n)
         gen_solver(n)
