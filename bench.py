@@ -103,30 +103,34 @@ def main():
 
         dist.init_process_group("nccl", device_id=dev)
 
+    from muzero_hanoi_amd import distributed as mdist
     from muzero_hanoi_amd import engine, rng
     from muzero_hanoi_amd.networks import MuZeroNet
 
     N, S, B = a.disks, a.sims, a.roots_per_gpu
+    GB = world * B  # global roots (weak scaling)
     torch.manual_seed(a.seed)
     net = MuZeroNet(3 * N, 6, 0.002, "cpu", TD_return=True)
-    flat = torch.from_numpy(engine.flat_weights(net.state_dict())).to(dev)
+    flat = engine.flat_weights(net.state_dict())
     if dist is not None:
-        dist.broadcast(flat, src=0)  # weights broadcast once (~0.5 MB)
+        flat = mdist.broadcast_weights(flat, dev)  # weights broadcast once (~0.5 MB)
     eng = engine.Engine(N, S, B, 33, device=local)
-    eng.load_weights(flat.cpu().numpy())
+    eng.load_weights(flat)
 
-    obs = torch.from_numpy(random_roots(N, B, a.seed * 1000 + rank)).to(dev)
-    noise, tie, u = rng.synthetic_draws(B, deterministic=False, alpha=0.25, seed=a.seed * 1000 + rank)
-    noise, tie, u = (torch.from_numpy(x).to(dev) for x in (noise, tie, u))
+    # inputs for the GLOBAL batch in global root order, then this rank's contiguous shard
+    sl = lambda x: mdist.shard(x, world, rank)
+    obs = torch.from_numpy(sl(random_roots(N, GB, a.seed))).to(dev)
+    noise, tie, u = rng.synthetic_draws(GB, deterministic=False, alpha=0.25, seed=a.seed)
+    noise, tie, u = (torch.from_numpy(sl(x)).to(dev) for x in (noise, tie, u))
     out = eng.alloc_search_outputs(B, S)
-    gathered = torch.empty((world * B, 6), dtype=torch.int32, device=dev) if (dist and not a.no_gather) else None
+    gather = dist is not None and not a.no_gather
     stream = torch.cuda.current_stream(dev)
 
     def step():
         eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, temperature=1.0, deterministic=False,
                    discount=0.8, eps=0.25, out=out)
-        if gathered is not None:
-            dist.all_gather_into_tensor(gathered, out["visits"])
+        if gather:
+            return mdist.gather_visits(out["visits"], GB, world)
 
     for _ in range(a.warmup):
         step()
@@ -147,8 +151,8 @@ def main():
         eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, temperature=1.0, deterministic=False,
                    discount=0.8, eps=0.25, out=out)
         evs[k][1].record(stream)
-        if gathered is not None:
-            dist.all_gather_into_tensor(gathered, out["visits"])
+        if gather:
+            mdist.gather_visits(out["visits"], GB, world)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()

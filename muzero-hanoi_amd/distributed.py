@@ -1,0 +1,47 @@
+"""Multi-GPU sharding of independent roots.
+
+Roots are independent, so the search shards with no data-path collective: rank r owns the
+contiguous slice [r*B/W, (r+1)*B/W) of the global batch.  Every random draw is made for the
+GLOBAL batch in global root order and then sliced, so results do not depend on the world size.
+The single exchange is an all_gather of the int32 visit histograms (RCCL over xGMI on the GPUs,
+gloo in the CPU tests); weights are broadcast once at start-up.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def shard_range(B, world, rank):
+    """contiguous, balanced shards: the first B % world ranks get one extra root"""
+    base, extra = divmod(B, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def shard(x, world, rank):
+    if x is None:
+        return None
+    s, e = shard_range(len(x), world, rank)
+    return x[s:e]
+
+
+def broadcast_weights(flat, device, src=0):
+    """weights broadcast once (~0.5 MB); returns a host numpy copy identical on every rank"""
+    t = torch.as_tensor(np.ascontiguousarray(flat, np.float32)).to(device)
+    dist.broadcast(t, src=src)
+    return t.cpu().numpy()
+
+
+def gather_visits(local, B, world):
+    """all_gather of per-rank [b_r, 6] int32 visit histograms -> global [B, 6] in root order.
+    Shards may differ by one root: each rank pads to the largest shard size."""
+    bmax = shard_range(B, world, 0)[1]  # rank 0 holds the largest shard
+    pad = torch.zeros((bmax, local.shape[1]), dtype=local.dtype, device=local.device)
+    pad[: local.shape[0]] = local
+    out = torch.empty((world * bmax, local.shape[1]), dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, pad)
+    parts = []
+    for r in range(world):
+        s, e = shard_range(B, world, r)
+        parts.append(out[r * bmax: r * bmax + (e - s)])
+    return torch.cat(parts)
