@@ -368,6 +368,24 @@ def gen_episode(name, n, s, max_steps, seed, episode, deterministic, wseed=0, td
     )
 
 
+def gen_checkpoint():
+    """A muzero_model.pt in the reference's format (training_main.py:91-103) after one Adam step,
+    plus the weights after the reference's own head ablation (acting_ablations.py:29-45)."""
+    sys.path.insert(0, os.path.join(REF, "acting_experiments"))
+    net = make_net(3, 2)
+    x = torch.zeros(4, 9)
+    x[:, 0] = 1
+    loss = net.represent(x).sum() + sum(p.sum() for p in net.prediction(net.represent(x)))
+    net.update(loss)
+    torch.save({"Muzero_net": net.state_dict(), "Net_optim": net.optimiser.state_dict()},
+               os.path.join(HERE, "muzero_model_N3.pt"))
+    torch.manual_seed(123)
+    net.policy_net.apply(net.reset_param)
+    net.rwd_net.apply(net.reset_param)
+    np.savez_compressed(os.path.join(HERE, "ablated_N3.npz"),
+                        **{k: v.numpy() for k, v in net.state_dict().items() if k.startswith(("policy", "rwd"))})
+
+
 EPISODE_CASES = [
     ("n3s25_t1", 3, 25, 40, 3, 1, False),
     ("n3s25_t05", 3, 25, 30, 5, 600, False),
@@ -376,6 +394,7 @@ EPISODE_CASES = [
 
 
 def main():
+    gen_checkpoint()
     for name, n, s, ms, seed, ep, det in EPISODE_CASES:
         gen_episode(name, n, s, ms, seed, ep, det)
     for n in (3, 4, 7):
