@@ -179,6 +179,7 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
     }
     rb.P64[c] = v;
   }
+  if (tid < R && tid >= nvalid) sm.act[tid] = 0;  // rows beyond the batch: any valid one-hot index
   floatx4 fa[16], fb[16];
   float ba[4], bb[4];
   if (!REPLAY && PF) mzh_mlp_fetch12<R>(sm, net, wave, lane, fa, ba, fb, bb);
@@ -216,6 +217,15 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
           path[r * PL] = (uint16_t)pick;
           st.pc[r][0] = MzhPathEnt{Wc, Rc, Nc};
         }
+        // every lane prefetches its own child's block (the selection's next level is one of
+        // them): the block's cache lines are in flight while this level's UCB/argmax completes
+        int pf0 = 0, pf1 = 0, pf2 = 0;
+        if (c < MZH_A && Xc >= 0) {
+          const int* q = reinterpret_cast<const int*>(tb + Xc);
+          pf0 = q[0];
+          pf1 = q[32];
+          pf2 = q[39];
+        }
         int nx = __shfl((Nc & 0xFFFF) | (Xc << 16), (lane & ~7) + pick);
         int depth = 1, e = 0;
         // deeper levels: tree blocks in HBM
@@ -228,12 +238,24 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
           Nc = 0;
           Wc = 0.0;
           Rc = 0.0f;
+          float Pc = 0.0f;
           if (c < MZH_A) {
             nxc = *reinterpret_cast<const int*>(&b->nx[c]);
-            Nc = nxc & 0xFFFF;
             Rc = b->R[c];
             Wc = b->W[c];
-            ucb = mzh_ucb(Nc, Wc, Rc, (double)b->P[c], p.np1, table[Np], disc, mmax, mmin);
+            Pc = b->P[c];
+          }
+          asm volatile("" ::"v"(pf0), "v"(pf1), "v"(pf2));  // retire the previous level's prefetch
+          if (c < MZH_A) {
+            const int xc = nxc >> 16;
+            if (xc >= 0) {
+              const int* q = reinterpret_cast<const int*>(tb + xc);
+              pf0 = q[0];
+              pf1 = q[32];
+              pf2 = q[39];
+            }
+            Nc = nxc & 0xFFFF;
+            ucb = mzh_ucb(Nc, Wc, Rc, (double)Pc, p.np1, table[Np], disc, mmax, mmin);
           }
           pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
           if (c == pick) {
@@ -243,6 +265,7 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
           nx = __shfl(nxc, (lane & ~7) + pick);
           depth++;
         }
+        asm volatile("" ::"v"(pf0), "v"(pf1), "v"(pf2));
         if (c == 0) {
           st.depth[r] = depth;
           st.leafE[r] = e;
@@ -250,6 +273,15 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
           st.steps[r] += depth;
           st.firstTie[r] = firstTie;
           st.extra[r] = extra;
+        }
+        if (!REPLAY) {
+          // MLP input for this root: the parent's latent (mcts.py:89-92) and the leaf's move
+          const float4* hsrc = reinterpret_cast<const float4*>(p.htree) + ((size_t)(root0 + r) * p.E + e) * 16 + c * 2;
+          const float4 h0 = hsrc[0], h1 = hsrc[1];
+          float* d = &sm.x[r * MZH_LD64 + c * 8];
+          d[0] = h0.x; d[1] = h0.y; d[2] = h0.z; d[3] = h0.w;
+          d[4] = h1.x; d[5] = h1.y; d[6] = h1.z; d[7] = h1.w;
+          if (c == 0) sm.act[r] = pick;
         }
       }
     }
@@ -259,16 +291,6 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
 
     // ---------------- Phase 2: expand via the network (mcts.py:88-106) ----------------
     if (!REPLAY) {
-      for (int i = tid; i < R * 16; i += MZH_THREADS) {
-        const int r = i >> 4, qd = i & 15;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (r < nvalid)
-          v = reinterpret_cast<const float4*>(p.htree)[((size_t)(root0 + r) * p.E + st.leafE[r]) * 16 + qd];
-        float* d = &sm.x[r * MZH_LD64 + qd * 4];
-        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-      }
-      if (tid < R) sm.act[tid] = tid < nvalid ? st.leafA[tid] : 0;
-      __syncthreads();
       MZH_STAMP(19);
       if (PF) {
         mzh_mlp_recurrent_body<R, PF>(sm, net, wave, lane, fa, ba, fb, bb);
