@@ -113,6 +113,36 @@ __device__ __forceinline__ float mzh_sum8(float v) {
   return v;
 }
 
+__device__ __forceinline__ double mzh_dpp_d(double v, int ctrl_sel) {
+  const long long b = __double_as_longlong(v);
+  const int lo = (int)(b & 0xFFFFFFFFll), hi = (int)(b >> 32);
+  int l2, h2;
+  switch (ctrl_sel) {
+    case 0:
+      l2 = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, false);
+      h2 = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false);
+      break;
+    case 1:
+      l2 = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xF, 0xF, false);
+      h2 = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xF, 0xF, false);
+      break;
+    default:
+      l2 = __builtin_amdgcn_mov_dpp(lo, 0x141, 0xF, 0xF, false);
+      h2 = __builtin_amdgcn_mov_dpp(hi, 0x141, 0xF, 0xF, false);
+      break;
+  }
+  return __longlong_as_double(((long long)h2 << 32) | (unsigned)l2);
+}
+// max / min over an aligned 8-lane group (exact: order-free)
+__device__ __forceinline__ void mzh_maxmin8d(double& mx, double& mn) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double tx = mzh_dpp_d(mx, i), tn = mzh_dpp_d(mn, i);
+    mx = tx > mx ? tx : mx;
+    mn = tn < mn ? tn : mn;
+  }
+}
+
 // logits_to_transformed_expected_value (networks.py:152-184); logits in LDS
 __device__ inline float mzh_logits_to_value(const float* l, int support) {
   if (support == 1) return l[0];
@@ -375,6 +405,18 @@ __device__ __forceinline__ void mzh_mma_store(const floatx4* f, const float* bv,
 }
 
 // normalize_h_state (networks.py:191-196): 8 lanes per row, 8 elements per lane.
+// a / b for a >= 0 and a normal b > 0, from y = RN(1/b) (Markstein: q = RN(a*y), the fma residual
+// is exact, one correction step gives RN(a/b)).  Exact unless the residual can underflow: `slow`
+// flags a != 0 with a or the quotient below 2^-100, and the caller redoes the wave with IEEE
+// division (tests/test_markstein.py checks the fp32 and fp64 forms against true division).
+__device__ __forceinline__ float mzh_fdiv(float a, float b, float y, bool& slow) {
+  const float q = a * y;
+  const float r = __builtin_fmaf(-q, b, a);
+  const float res = __builtin_fmaf(r, y, q);
+  slow |= (a != 0.0f) & ((a < 0x1p-100f) | (res < 0x1p-100f));
+  return res;
+}
+
 template <int R>
 __device__ __forceinline__ void mzh_normalize_par(const float* src, float* dst, int tid) {
 #pragma unroll
@@ -394,83 +436,108 @@ __device__ __forceinline__ void mzh_normalize_par(const float* src, float* dst, 
       mx = mzh_max8(mx);
       const float d = (mx - mn) + 9.999999939225290290778502821922302246094e-09f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) dst[row * MZH_LD64 + part * 8 + i] = (v[i] - mn) / d;
+      for (int i = 0; i < 8; ++i) v[i] = v[i] - mn;
+      const float y = 1.0f / d;
+      bool slow = false;
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = mzh_fdiv(v[i], d, y, slow);
+      if (__builtin_expect(__ballot(slow) != 0, 0)) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = v[i] / d;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dst[row * MZH_LD64 + part * 8 + i] = o[i];
     }
   }
 }
 
-// Heads (networks.py:83,109,152-189): 8 lanes per (row, head).  Lane q owns logits k = q + 8i;
-// max / exp / divide are lane-parallel, and both 33-term sums use the fixed order of sum8_tree
-// in the oracle: sequential per-lane partials combined by the DPP tree (mzh_sum8).
-template <int R>
-__device__ __forceinline__ void mzh_value_head8(const float* l, int q, float* out) {
-  float e[5];
-  float m = -__builtin_inff();
-#pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const int k = q + 8 * i;
-    e[i] = k < 33 ? l[k] : -__builtin_inff();
-    m = e[i] > m ? e[i] : m;
-  }
-  m = mzh_max8(m);
-#pragma unroll
-  for (int i = 0; i < 5; ++i) e[i] = (q + 8 * i < 33) ? mzh_expf(e[i] - m) : 0.0f;
-  float a = e[0];
-#pragma unroll
-  for (int i = 1; i < 4; ++i) a = a + e[i];
-  if (q == 0) a = a + e[4];
-  const float s = mzh_sum8(a);
-  float x = 0.0f;
-#pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const int k = q + 8 * i;
-    if (k < 33) {
-      const float pk = e[i] / s;
-      const float prod = pk * (float)(k - 16);
-      x = i == 0 ? prod : x + prod;
-    }
-  }
-  x = mzh_sum8(x);
-  if (q == 0) *out = mzh_signed_parabolic(x);
-}
-
+// Heads (networks.py:83,109,152-189): 8 lanes per row; the value and reward heads of a row run
+// interleaved on the same lanes (independent chains), the policy softmax alongside.  Lane q owns
+// logits k = q + 8i; max / exp / divide are lane-parallel, and both 33-term sums use the fixed
+// order of sum8_tree in the oracle: sequential per-lane partials combined by the DPP tree.
 template <int R>
 __device__ __forceinline__ void mzh_heads_par(MlpSmem<R>& sm, float* scratch, int support, bool recurrent, int tid) {
   (void)scratch;
-  const int g = tid >> 3, q = tid & 7;  // 32 groups of 8 lanes over 256 threads
-  // value heads, then reward heads (recurrent), 32 rows per pass
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    const bool isr = pass == 1;
-    if (isr && !recurrent) {
-      if (tid < R) sm.reward[tid] = 0.0f;
-      continue;
+  const int row = tid >> 3, q = tid & 7;  // 32 rows of 8 lanes over 256 threads
+  if (row >= R) return;
+  const float lg = q < MZH_A ? sm.lpol[row * MZH_LDPOL + q] : -__builtin_inff();
+  if (support == 1) {
+    if (q == 0) {
+      sm.value[row] = sm.lval[row * MZH_LDSUP];
+      sm.reward[row] = recurrent ? sm.lrwd[row * MZH_LDSUP] : 0.0f;
     }
+  }
+  const int nh = support == 1 ? 0 : (recurrent ? 2 : 1);
+  const float* lv[2] = {sm.lval + row * MZH_LDSUP, sm.lrwd + row * MZH_LDSUP};
+  float e[2][5], m[2];
 #pragma unroll
-    for (int row0 = 0; row0 < R; row0 += 32) {
-      const int row = row0 + g;
-      if (row < R) {
-        const float* l = (isr ? sm.lrwd : sm.lval) + row * MZH_LDSUP;
-        float* out = isr ? &sm.reward[row] : &sm.value[row];
-        if (support == 1) {
-          if (q == 0) *out = l[0];
-        } else {
-          mzh_value_head8<R>(l, q, out);
-        }
+  for (int h = 0; h < 2; ++h) {
+    m[h] = -__builtin_inff();
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int k = q + 8 * i;
+      e[h][i] = (h < nh && k < 33) ? lv[h][k] : -__builtin_inff();
+      m[h] = e[h][i] > m[h] ? e[h][i] : m[h];
+    }
+  }
+  const float mp = mzh_max8(lg);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) m[h] = mzh_max8(m[h]);
+  const float ep = q < MZH_A ? mzh_expf(lg - mp) : 0.0f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 5; ++i) e[h][i] = (q + 8 * i < 33) ? mzh_expf(e[h][i] - m[h]) : 0.0f;
+  float sh[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float a = e[h][0];
+#pragma unroll
+    for (int i = 1; i < 4; ++i) a = a + e[h][i];
+    if (q == 0) a = a + e[h][4];
+    sh[h] = a;
+  }
+  const float sp = mzh_sum8(ep);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) sh[h] = mzh_sum8(sh[h]);
+  // probabilities: Markstein division from one reciprocal per head, IEEE fallback when flagged
+  bool slow = false;
+  float pk[2][5];
+  const float yp = 1.0f / sp;
+  float pp = mzh_fdiv(ep, sp, yp, slow);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float y = 1.0f / sh[h];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) pk[h][i] = mzh_fdiv(e[h][i], sh[h], y, slow);
+  }
+  if (__builtin_expect(__ballot(slow) != 0, 0)) {
+    pp = ep / sp;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 5; ++i) pk[h][i] = e[h][i] / sh[h];
+  }
+  if (q < MZH_A) sm.pi[row * 8 + q] = pp;
+  float x[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    x[h] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int k = q + 8 * i;
+      if (k < 33) {
+        const float prod = pk[h][i] * (float)(k - 16);
+        x[h] = i == 0 ? prod : x[h] + prod;
       }
     }
   }
-  // policy softmax: 8 lanes per row, lanes 0..5 hold one logit each
 #pragma unroll
-  for (int row0 = 0; row0 < R; row0 += 32) {
-    const int row = row0 + g;
-    if (row < R) {
-      const float lg = q < MZH_A ? sm.lpol[row * MZH_LDPOL + q] : -__builtin_inff();
-      const float m = mzh_max8(lg);
-      const float e = q < MZH_A ? mzh_expf(lg - m) : 0.0f;
-      const float s = mzh_sum8(e);
-      if (q < MZH_A) sm.pi[row * 8 + q] = e / s;
-    }
+  for (int h = 0; h < 2; ++h) x[h] = mzh_sum8(x[h]);
+  if (q == 0 && nh > 0) {
+    sm.value[row] = mzh_signed_parabolic(x[0]);
+    sm.reward[row] = nh > 1 ? mzh_signed_parabolic(x[1]) : 0.0f;
   }
 }
 
@@ -540,7 +607,8 @@ __device__ __forceinline__ void mzh_mlp_fetch12(MlpSmem<R>& sm, const MzhNet& ne
 
 template <int R, bool NEXT>
 __device__ __forceinline__ void mzh_mlp_recurrent_body(MlpSmem<R>& sm, const MzhNet& net, int wave_in, int lane,
-                                                       floatx4* fa, float* ba, floatx4* fb, float* bb) {
+                                                       floatx4* fa, float* ba, floatx4* fb, float* bb,
+                                                       const float* onehot) {
   constexpr int MT = R / 16;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(wave_in);  // wave-uniform -> chunk descriptors in SGPRs
@@ -555,7 +623,7 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(MlpSmem<R>& sm, const Mzh
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          oh[(q * MT + m) * 4 + i] = net.dyn0_onehot[sm.act[m * 16 + g * 4 + i] * MZH_F + (wave * 4 + q) * 16 + r];
+          oh[(q * MT + m) * 4 + i] = onehot[sm.act[m * 16 + g * 4 + i] * MZH_F + (wave * 4 + q) * 16 + r];
     MZH_STAMP(0);
     mzh_mma_store<MT, 4, 4, true>(fa, ba, mzh_chunk(net.dyn0, wave * 4, 4, sm.hidP, MZH_LD256), sm.x, MZH_LD64, true, oh,
                             lane);  // dyn0 + one-hot + bias, relu
@@ -604,5 +672,5 @@ __device__ void mzh_mlp_recurrent(MlpSmem<R>& sm, const MzhNet& net, int wave, i
   floatx4 fa[16], fb[16];
   float ba[4], bb[4];
   mzh_mlp_fetch12<R>(sm, net, wave, lane, fa, ba, fb, bb);
-  mzh_mlp_recurrent_body<R, false>(sm, net, wave, lane, fa, ba, fb, bb);
+  mzh_mlp_recurrent_body<R, false>(sm, net, wave, lane, fa, ba, fb, bb, net.dyn0_onehot);
 }

@@ -13,19 +13,22 @@
 #include "mzh_internal.h"
 
 // ------------------------------------------------------------------------------------------
-// tree block: the 6 children of one expanded node (+2 pad lanes)
+// tree block: the 6 children of one expanded node in exactly one 128-byte cache line, so a
+// selection level touches one line (L2-resident hot path)
 // ------------------------------------------------------------------------------------------
 struct MzhNX {
   uint16_t N;  // child visit count (node.py:21)
   int16_t X;   // expanded-node index of the child, -1 = not expanded (node.py:19 is_expanded)
 };
-struct __align__(16) MzhBlock {
-  MzhNX nx[8];  // N and X adjacent: one dword load per child in selection
-  float R[8];   // child reward (python float of an fp32 value, node.py:25)
-  float P[8];   // child prior, fp32 (node.py:16)
-  double W[8];  // child summed value, fp64 (node.py:22)
+struct __align__(128) MzhBlock {
+  MzhNX nx[6];  // N and X adjacent: one dword load per child in selection
+  float R[6];   // child reward (python float of an fp32 value, node.py:25)
+  float P[6];   // child prior, fp32 (node.py:16)
+  double W[6];  // child summed value, fp64 (node.py:22)
+  uint32_t pad[2];
 };
-static_assert(sizeof(MzhBlock) == 160, "block layout");
+static_assert(sizeof(MzhBlock) == 128, "block layout");
+static_assert(__builtin_offsetof(MzhBlock, W) == 72, "block layout");
 
 // the root's 6 children live in LDS for the whole search (every simulation starts there)
 struct MzhRootBlk {
@@ -62,17 +65,28 @@ struct SearchSmem {
   int pad_[R];
 };
 
-__device__ __forceinline__ double mzh_normalize(double v, double mx, double mn) {
-  if (mx > mn) return (v - mn) / (mx - mn);  // utils_mcts.py:12-16
-  return v;
+// a / b correctly rounded from y = RN(1/b) (Markstein: q = RN(a*y) is within one ulp, the fma
+// residual is exact, and one correction step rounds to RN(a/b)); 3 fp64 ops instead of the
+// ~12-op div_scale/rcp/fmas/fixup sequence on the select chain.  Equal to `a / b` for every
+// finite non-subnormal quotient; checked against true division in tests/test_markstein.py.
+__device__ __forceinline__ double mzh_div(double a, double b, double y) {
+  const double q = a * y;
+  const double r = __builtin_fma(-q, b, a);
+  return __builtin_fma(r, y, q);
 }
 
-// ucb = fl32(Q) + fl32(U) for one child (node.py:90-123); `tnp` = table[N_parent]
+// MinMaxStats.normalize (utils_mcts.py:12-16) with den = max - min, dinv = RN(1/den)
+__device__ __forceinline__ double mzh_normalize(double v, bool has, double mn, double den, double dinv) {
+  return has ? mzh_div(v - mn, den, dinv) : v;
+}
+
+// ucb = fl32(Q) + fl32(U) for one child (node.py:90-123); `tnp` = table[N_parent], inv[k] = RN(1/k)
 __device__ __forceinline__ float mzh_ucb(int Nc, double Wc, float Rc, double P64, bool p64_semantics, double tnp,
-                                         double disc, double mmax, double mmin) {
+                                         double disc, bool has, double mn, double den, double dinv,
+                                         const double* inv) {
   float q32 = 0.0f;
-  if (Nc > 0) q32 = (float)mzh_normalize((double)Rc + disc * (Wc / (double)Nc), mmax, mmin);
-  const double w = tnp / (double)(Nc + 1);
+  if (Nc > 0) q32 = (float)mzh_normalize((double)Rc + disc * mzh_div(Wc, (double)Nc, inv[Nc]), has, mn, den, dinv);
+  const double w = mzh_div(tnp, (double)(Nc + 1), inv[Nc + 1]);
   // np.float64 priors (Dirichlet-mixed root) or NumPy-1 promotion: fl32(fl64(prior * w));
   // NumPy-2 with np.float32 priors: fl32(prior * fl32(w))
   const float u32 = p64_semantics ? (float)(P64 * w) : (float)P64 * (float)w;
@@ -108,7 +122,7 @@ __device__ __forceinline__ double mzh_pow(double x, double e) {
 
 // R = 32: one workgroup per CU (all 512 registers per lane); R = 16: two co-resident workgroups
 // per CU (<= 256 registers), so one workgroup's latency-bound tree phase overlaps the other's MFMAs.
-template <int R, bool REPLAY>
+template <int R, bool REPLAY, bool OHL>
 __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kernel(MzhNet net, MzhSearchParams p) {
   constexpr int DC = SearchSmem<R>::DC;
   constexpr bool PF = R == 32;  // keep the next step's first weight chunks in flight across the tree phase
@@ -116,7 +130,10 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
   MlpSmem<R>& sm = *reinterpret_cast<MlpSmem<R>*>(smem_raw);
   SearchSmem<R>& st = *reinterpret_cast<SearchSmem<R>*>(smem_raw + sizeof(MlpSmem<R>));
   double* table = reinterpret_cast<double*>(smem_raw + sizeof(MlpSmem<R>) + sizeof(SearchSmem<R>));
-  uint16_t* path = reinterpret_cast<uint16_t*>(table + ((p.S + 2 + 1) & ~1));
+  double* inv = table + (p.S + 3);  // inv[k] = RN(1/k), k <= S + 2
+  uint16_t* path = reinterpret_cast<uint16_t*>(table + 2 * (p.S + 3));
+  // OHL: the dynamics one-hot columns (6 x 256 floats) live in LDS (when the launcher finds room)
+  float* ohl = reinterpret_cast<float*>(path + ((R * (p.S + 1) + 7) & ~7));
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int root0 = blockIdx.x * R;
@@ -126,7 +143,12 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
   const double disc = p.discount;
   const bool noised = p.noise != nullptr;
 
-  for (int i = tid; i < S + 2; i += MZH_THREADS) table[i] = p.table[i];
+  if (OHL)
+    for (int i = tid; i < MZH_A * MZH_F; i += MZH_THREADS) ohl[i] = net.dyn0_onehot[i];
+  for (int i = tid; i < S + 3; i += MZH_THREADS) {
+    table[i] = i < S + 2 ? p.table[i] : 0.0;
+    inv[i] = 1.0 / (double)i;  // IEEE division: correctly rounded
+  }
   if (tid < R) {
     const int r = tid;
     st.rootN[r] = 0;
@@ -194,6 +216,9 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
       if (r < nvalid) {
         const MzhBlock* tb = reinterpret_cast<const MzhBlock*>(p.tree) + (size_t)(root0 + r) * p.E;
         const double mmax = st.mm[r][0], mmin = st.mm[r][1];
+        const bool has = mmax > mmin;
+        const double den = mmax - mmin;
+        const double dinv = has ? 1.0 / den : 0.0;
         int firstTie = st.firstTie[r];
         int extra = st.extra[r];
         const int tie = p.tie_idx ? p.tie_idx[root0 + r] : 0;
@@ -208,7 +233,7 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
           Xc = rb.X[c];
           Wc = rb.W[c];
           Rc = rb.R[c];
-          ucb = mzh_ucb(Nc, Wc, Rc, rb.P64[c], noised || p.np1, table[st.rootN[r]], disc, mmax, mmin);
+          ucb = mzh_ucb(Nc, Wc, Rc, rb.P64[c], noised || p.np1, table[st.rootN[r]], disc, has, mmin, den, dinv, inv);
         }
         int pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
         // the picking lane records the path entry and its own statistics; one shuffle of the
@@ -219,44 +244,31 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
         }
         // every lane prefetches its own child's block (the selection's next level is one of
         // them): the block's cache lines are in flight while this level's UCB/argmax completes
-        int pf0 = 0, pf1 = 0, pf2 = 0;
-        if (c < MZH_A && Xc >= 0) {
-          const int* q = reinterpret_cast<const int*>(tb + Xc);
-          pf0 = q[0];
-          pf1 = q[32];
-          pf2 = q[39];
-        }
+        // (unconditional loads -- a lane without a child re-reads a valid block -- so the
+        // compiler can count outstanding loads and wait only for the ones a level needs)
+        int pf0 = *reinterpret_cast<const int*>(tb + (Xc >= 0 ? Xc : 0));
         int nx = __shfl((Nc & 0xFFFF) | (Xc << 16), (lane & ~7) + pick);
         int depth = 1, e = 0;
-        // deeper levels: tree blocks in HBM
+        // deeper levels: tree blocks in HBM (L2); lanes 6, 7 re-read slot 5 and act as
+        // unexpanded, unvisited pads (N = 0, X = -1)
+        const int cs = c < MZH_A ? c : MZH_A - 1;
         while ((nx >> 16) >= 0) {
           e = nx >> 16;
           const int Np = nx & 0xFFFF;
           const MzhBlock* b = tb + e;
-          ucb = -__builtin_inff();
-          int nxc = (int)0xFFFF0000;
-          Nc = 0;
-          Wc = 0.0;
-          Rc = 0.0f;
-          float Pc = 0.0f;
-          if (c < MZH_A) {
-            nxc = *reinterpret_cast<const int*>(&b->nx[c]);
-            Rc = b->R[c];
-            Wc = b->W[c];
-            Pc = b->P[c];
-          }
-          asm volatile("" ::"v"(pf0), "v"(pf1), "v"(pf2));  // retire the previous level's prefetch
-          if (c < MZH_A) {
-            const int xc = nxc >> 16;
-            if (xc >= 0) {
-              const int* q = reinterpret_cast<const int*>(tb + xc);
-              pf0 = q[0];
-              pf1 = q[32];
-              pf2 = q[39];
-            }
-            Nc = nxc & 0xFFFF;
-            ucb = mzh_ucb(Nc, Wc, Rc, (double)Pc, p.np1, table[Np], disc, mmax, mmin);
-          }
+          int nxc = *reinterpret_cast<const int*>(&b->nx[cs]);
+          Rc = b->R[cs];
+          Wc = b->W[cs];
+          const float Pc = b->P[cs];
+          if (c >= MZH_A) nxc = (int)0xFFFF0000;
+          // retire the previous level's prefetch (older than this level's block loads, so no
+          // extra wait) -- keeps it in flight inside the loop
+          asm volatile("" ::"v"(pf0));
+          const int xc = nxc >> 16;
+          pf0 = *reinterpret_cast<const int*>(tb + (xc >= 0 ? xc : e));
+          Nc = nxc & 0xFFFF;
+          ucb = c < MZH_A ? mzh_ucb(Nc, Wc, Rc, (double)Pc, p.np1, table[Np], disc, has, mmin, den, dinv, inv)
+                          : -__builtin_inff();
           pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
           if (c == pick) {
             path[r * PL + depth] = (uint16_t)(e * 8 + pick);
@@ -265,7 +277,7 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
           nx = __shfl(nxc, (lane & ~7) + pick);
           depth++;
         }
-        asm volatile("" ::"v"(pf0), "v"(pf1), "v"(pf2));
+        asm volatile("" ::"v"(pf0));
         if (c == 0) {
           st.depth[r] = depth;
           st.leafE[r] = e;
@@ -276,11 +288,11 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
         }
         if (!REPLAY) {
           // MLP input for this root: the parent's latent (mcts.py:89-92) and the leaf's move
-          const float4* hsrc = reinterpret_cast<const float4*>(p.htree) + ((size_t)(root0 + r) * p.E + e) * 16 + c * 2;
-          const float4 h0 = hsrc[0], h1 = hsrc[1];
+          const floatx4* hsrc = reinterpret_cast<const floatx4*>(p.htree) + ((size_t)(root0 + r) * p.E + e) * 16 + c * 2;
+          const floatx4 h0 = hsrc[0], h1 = hsrc[1];
           float* d = &sm.x[r * MZH_LD64 + c * 8];
-          d[0] = h0.x; d[1] = h0.y; d[2] = h0.z; d[3] = h0.w;
-          d[4] = h1.x; d[5] = h1.y; d[6] = h1.z; d[7] = h1.w;
+          d[0] = h0[0]; d[1] = h0[1]; d[2] = h0[2]; d[3] = h0[3];
+          d[4] = h1[0]; d[5] = h1[1]; d[6] = h1[2]; d[7] = h1[3];
           if (c == 0) sm.act[r] = pick;
         }
       }
@@ -293,19 +305,11 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
     if (!REPLAY) {
       MZH_STAMP(19);
       if (PF) {
-        mzh_mlp_recurrent_body<R, PF>(sm, net, wave, lane, fa, ba, fb, bb);
+        mzh_mlp_recurrent_body<R, PF>(sm, net, wave, lane, fa, ba, fb, bb, OHL ? ohl : net.dyn0_onehot);
       } else {
         mzh_mlp_recurrent<R>(sm, net, wave, lane);
       }
       MZH_STAMP(20);
-      for (int i = tid; i < R * 16; i += MZH_THREADS) {
-        const int r = i >> 4, qd = i & 15;
-        if (r < nvalid) {
-          const float* src = &sm.x[r * MZH_LD64 + qd * 4];
-          reinterpret_cast<float4*>(p.htree)[((size_t)(root0 + r) * p.E + s + 1) * 16 + qd] =
-              make_float4(src[0], src[1], src[2], src[3]);
-        }
-      }
     } else {
       if (tid < R * 8) {
         const int r = tid >> 3, c = tid & 7;
@@ -329,11 +333,22 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
         MzhBlock* tb = reinterpret_cast<MzhBlock*>(p.tree) + (size_t)(root0 + r) * p.E;
         MzhRootBlk& rb = st.root[r];
         const int enew = s + 1;
+        if (!REPLAY) {
+          // the new node's latent (read back when one of its children is expanded -- usually
+          // within a few simulations on the deepening path, so it stays cacheable)
+          const float* src = &sm.x[r * MZH_LD64 + c * 8];
+          floatx4* dst = reinterpret_cast<floatx4*>(p.htree) + ((size_t)(root0 + r) * p.E + enew) * 16 + c * 2;
+          const floatx4 v0 = {src[0], src[1], src[2], src[3]}, v1 = {src[4], src[5], src[6], src[7]};
+          dst[0] = v0;
+          dst[1] = v1;
+        }
         MzhBlock* nb = tb + enew;  // the new expanded node's 6 children (node.py:44-49)
-        *reinterpret_cast<uint32_t*>(&nb->nx[c]) = 0xFFFF0000u;  // N = 0, X = -1
-        nb->R[c] = 0.0f;
-        nb->P[c] = c < MZH_A ? sm.pi[r * 8 + c] : 0.0f;
-        nb->W[c] = 0.0;
+        if (c < MZH_A) {
+          *reinterpret_cast<uint32_t*>(&nb->nx[c]) = 0xFFFF0000u;  // N = 0, X = -1
+          nb->R[c] = 0.0f;
+          nb->P[c] = sm.pi[r * 8 + c];
+          nb->W[c] = 0.0;
+        }
         const int le = st.leafE[r], la = st.leafA[r], depth = st.depth[r];
         const float rew = sm.reward[r];
         double lmax = -__builtin_inf(), lmin = __builtin_inf();
@@ -355,7 +370,7 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
             const int N = tb[e].nx[a].N + 1;
             tb[e].W[a] = W;
             tb[e].nx[a].N = (uint16_t)N;
-            const double q = rw + disc * (W / (double)N);
+            const double q = rw + disc * mzh_div(W, (double)N, inv[N]);
             lmax = q > lmax ? q : lmax;
             lmin = q < lmin ? q : lmin;
             v = rw + disc * v;
@@ -374,7 +389,7 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
           const int N = st.rootN[r] + 1;
           st.rootW[r] = W;
           st.rootN[r] = N;
-          const double q = 0.0 + disc * (W / (double)N);  // root rwd = 0.0
+          const double q = 0.0 + disc * mzh_div(W, (double)N, inv[N]);  // root rwd = 0.0
           lmax = q > lmax ? q : lmax;
           lmin = q < lmin ? q : lmin;
         }
@@ -394,16 +409,11 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
             tb[e].W[a] = W;
             tb[e].nx[a].N = (uint16_t)N;
           }
-          const double q = rw + disc * (W / (double)N);
+          const double q = rw + disc * mzh_div(W, (double)N, inv[N]);
           lmax = q > lmax ? q : lmax;
           lmin = q < lmin ? q : lmin;
         }
-#pragma unroll
-        for (int o = 1; o < 8; o <<= 1) {
-          const double tx = __shfl_xor(lmax, o), tn = __shfl_xor(lmin, o);
-          lmax = tx > lmax ? tx : lmax;
-          lmin = tn < lmin ? tn : lmin;
-        }
+        mzh_maxmin8d(lmax, lmin);
         if (c == 0) {
           const double mx = st.mm[r][0], mn = st.mm[r][1];
           st.mm[r][0] = lmax > mx ? lmax : mx;
@@ -521,29 +531,37 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_recurrent_kernel(MzhNet ne
 // launchers
 // ------------------------------------------------------------------------------------------
 template <int R>
-static size_t search_smem_bytes(int S) {
+static size_t search_smem_bytes(int S, bool ohl) {
   size_t b = sizeof(MlpSmem<R>) + sizeof(SearchSmem<R>);
-  b += sizeof(double) * (size_t)((S + 2 + 1) & ~1);
-  b += sizeof(uint16_t) * (size_t)R * (size_t)(S + 1);
+  b += sizeof(double) * 2 * (size_t)(S + 3);
+  b += sizeof(uint16_t) * (size_t)((R * (S + 1) + 7) & ~7);
+  if (ohl) b += sizeof(float) * MZH_A * MZH_F;
   return (b + 15) & ~(size_t)15;
 }
 
-size_t mzh_search_smem_bytes(int R, int S) { return R == 32 ? search_smem_bytes<32>(S) : search_smem_bytes<16>(S); }
+static const size_t kLdsBytes = 163840;  // 160 KB per CU (gfx950)
 
-template <int R, bool REPLAY>
+// the minimum LDS a search launch needs at this R (one-hot columns left in HBM)
+size_t mzh_search_smem_bytes(int R, int S) { return R == 32 ? search_smem_bytes<32>(S, false) : search_smem_bytes<16>(S, false); }
+
+template <int R, bool REPLAY, bool OHL>
 static hipError_t launch_search_t(const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
-  const size_t smem = search_smem_bytes<R>(p.S);
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mzh_search_kernel<R, REPLAY>),
+  const size_t smem = search_smem_bytes<R>(p.S, OHL);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mzh_search_kernel<R, REPLAY, OHL>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
   const int grid = (p.B + R - 1) / R;
-  hipLaunchKernelGGL((mzh_search_kernel<R, REPLAY>), dim3(grid), dim3(MZH_THREADS), smem, stream, net, p);
+  hipLaunchKernelGGL((mzh_search_kernel<R, REPLAY, OHL>), dim3(grid), dim3(MZH_THREADS), smem, stream, net, p);
   return hipGetLastError();
 }
 
 hipError_t mzh_launch_search(int R, bool replay, const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
-  if (R == 32) return replay ? launch_search_t<32, true>(net, p, stream) : launch_search_t<32, false>(net, p, stream);
-  return replay ? launch_search_t<16, true>(net, p, stream) : launch_search_t<16, false>(net, p, stream);
+  if (R == 32) {
+    if (replay) return launch_search_t<32, true, false>(net, p, stream);
+    if (search_smem_bytes<32>(p.S, true) <= kLdsBytes) return launch_search_t<32, false, true>(net, p, stream);
+    return launch_search_t<32, false, false>(net, p, stream);
+  }
+  return replay ? launch_search_t<16, true, false>(net, p, stream) : launch_search_t<16, false, false>(net, p, stream);
 }
 
 template <int R>

@@ -339,6 +339,51 @@ void orc_recurrent_inference(const float* flat, int in_dim, int support, int B, 
 #define PB_C_INIT 1.25  /* mcts.py:25 */
 
 /* (log((N + base + 1) / base) + init) * sqrt(N)   -- node.py:114-121 up to the "/ (child.N+1)" */
+/* Property check for the device's division (csrc/mzh_search.hip mzh_div): a / b computed as
+ * q = a*y, r = fma(-q, b, a), q' = fma(r, y, q) with y = RN(1/b) must equal IEEE a / b.  Runs n
+ * random trials over the select/backup operand domains (W / N and table[Np] / (N + 1) with integer
+ * N in [1, 64]; normalise's (v - min) / (max - min) with real denominators) and returns the number
+ * of mismatches (test infrastructure only, not part of the reference algorithm). */
+static uint64_t mk_s;
+static uint64_t mk_next(void) {
+  mk_s ^= mk_s << 13;
+  mk_s ^= mk_s >> 7;
+  mk_s ^= mk_s << 17;
+  return mk_s;
+}
+static double mk_unit(void) { return (double)(mk_next() >> 11) * (1.0 / 9007199254740992.0); }
+static double mk_rand_exp(int lo, int span) {
+  uint64_t u = mk_next();
+  u &= ~(0xfffull << 52);
+  u |= ((uint64_t)(1023 + lo + (int)(mk_next() % (uint64_t)span))) << 52;
+  double d;
+  memcpy(&d, &u, 8);
+  return d;
+}
+long orc_markstein_mismatches(long n, uint64_t seed) {
+  long bad = 0;
+  mk_s = seed ? seed : 88172645463325252ull;
+  for (long i = 0; i < n; ++i) {
+    double a, b;
+    if (i & 1) {
+      b = (double)(1 + (int)(mk_next() % 64));
+      switch (mk_next() % 3) {
+        case 0: a = (mk_unit() * 2 - 1) * 200.0; break;
+        case 1: a = ldexp(mk_unit() * 2 - 1, (int)(mk_next() % 60) - 30); break;
+        default: a = mk_rand_exp(-20, 40); break;
+      }
+    } else {
+      b = (mk_next() & 1) ? mk_unit() * 10 + 1e-9 : mk_rand_exp(-15, 30);
+      a = (mk_next() & 1) ? (mk_unit() * 2 - 1) * ldexp(1.0, (int)(mk_next() % 20) - 10) : mk_rand_exp(-15, 30);
+    }
+    const double y = 1.0 / b;
+    const double q = a * y;
+    const double r = fma(-q, b, a);
+    if (fma(r, y, q) != a / b) ++bad;
+  }
+  return bad;
+}
+
 double orc_ucb_table(int n) {
   return (log((double)(n + PB_C_BASE + 1) / (double)PB_C_BASE) + PB_C_INIT) * sqrt((double)n);
 }

@@ -43,6 +43,8 @@ def lib():
         L.orc_signed_parabolic.argtypes = [ctypes.c_float]
         L.orc_logits_to_value.restype = ctypes.c_float
         L.orc_logits_to_value.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.orc_markstein_mismatches.restype = ctypes.c_long
+        L.orc_markstein_mismatches.argtypes = [ctypes.c_long, ctypes.c_uint64]
         L.orc_ucb_table.restype = ctypes.c_double
         L.orc_ucb_table.argtypes = [ctypes.c_int]
         L.orc_hanoi_solver.restype = ctypes.c_long
