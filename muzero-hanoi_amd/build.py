@@ -29,11 +29,13 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose=False, force=False, diag=False):
-    """diag=True builds libmzh_diag.so with -DMZH_STAMPS (in-kernel phase stamps; never shipped)."""
-    obj_dir = OBJ + ("_diag" if diag else "")
-    lib_path = LIB.replace("libmzh.so", "libmzh_diag.so") if diag else LIB
-    flags = FLAGS + (["-DMZH_STAMPS"] if diag else [])
+def build(verbose=False, force=False, diag=False, tag="", defines=()):
+    """diag=True builds libmzh_diag.so with -DMZH_STAMPS (in-kernel phase stamps; never shipped).
+    tag/defines: an A/B variant of the diagnostic build (libmzh_diag_<tag>.so with -D<defines>)."""
+    sfx = ("_diag" if diag else "") + (f"_{tag}" if tag else "")
+    obj_dir = OBJ + sfx
+    lib_path = LIB.replace("libmzh.so", f"libmzh{sfx}.so")
+    flags = FLAGS + (["-DMZH_STAMPS"] if diag else []) + [f"-D{d}" for d in defines]
     os.makedirs(obj_dir, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     headers.append(os.path.join(REPO, "include", "mzh.h"))
@@ -64,4 +66,11 @@ def build(verbose=False, force=False, diag=False):
 
 
 if __name__ == "__main__":
-    print(build(verbose=True, force="--force" in sys.argv, diag="--diag" in sys.argv))
+    # --variant tag=DEF1,DEF2 : diagnostic A/B build libmzh_diag_<tag>.so
+    var = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--variant=")]
+    if var:
+        tag, defs = var[0].split("=", 1) if "=" in var[0] else (var[0], "")
+        print(build(verbose=True, force="--force" in sys.argv, diag=True, tag=tag,
+                    defines=[d for d in defs.split(",") if d]))
+    else:
+        print(build(verbose=True, force="--force" in sys.argv, diag="--diag" in sys.argv))

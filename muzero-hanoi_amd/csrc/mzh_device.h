@@ -24,7 +24,7 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 // Diagnostic phase stamps (only in the -DMZH_STAMPS build, libmzh_diag.so; never in libmzh.so).
 // Lane 0 of every wave accumulates s_memtime deltas per phase into mzh_stamp_acc[wave][phase].
 // ------------------------------------------------------------------------------------------
-#define MZH_NSTAMP 24
+#define MZH_NSTAMP 32
 #ifdef MZH_STAMPS
 __device__ unsigned long long mzh_stamp_acc[8][MZH_NSTAMP];
 #define MZH_STAMP_DECL unsigned long long mzh_t_prev = __builtin_amdgcn_s_memtime();
@@ -37,9 +37,31 @@ __device__ unsigned long long mzh_stamp_acc[8][MZH_NSTAMP];
     mzh_t_prev = t_;                                                                        \
     __builtin_amdgcn_sched_barrier(0);                                                      \
   } while (0)
+// register-accumulated stamps for divergent loops (flushed once by the first active lane)
+#define MZH_LSTAMP_DECL                                         \
+  unsigned long long mzh_lt_prev = __builtin_amdgcn_s_memtime(); \
+  unsigned long long mzh_lacc[5] = {0, 0, 0, 0, 0};
+#define MZH_LSTAMP(i)                                         \
+  do {                                                        \
+    __builtin_amdgcn_sched_barrier(0);                        \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();     \
+    mzh_lacc[i] += t_ - mzh_lt_prev;                          \
+    mzh_lt_prev = t_;                                         \
+    __builtin_amdgcn_sched_barrier(0);                        \
+  } while (0)
+#define MZH_LSTAMP_COUNT() (mzh_lacc[4] += 1)
+#define MZH_LSTAMP_FLUSH(base)                                                                  \
+  do {                                                                                          \
+    if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1 && blockIdx.x == 0)        \
+      for (int i_ = 0; i_ < 5; ++i_) atomicAdd(&mzh_stamp_acc[threadIdx.x >> 6][(base) + i_], mzh_lacc[i_]); \
+  } while (0)
 #else
 #define MZH_STAMP_DECL
 #define MZH_STAMP(ph) do {} while (0)
+#define MZH_LSTAMP_DECL
+#define MZH_LSTAMP(i) do {} while (0)
+#define MZH_LSTAMP_COUNT() do {} while (0)
+#define MZH_LSTAMP_FLUSH(base) do {} while (0)
 #endif
 
 // ------------------------------------------------------------------------------------------
@@ -318,14 +340,13 @@ __device__ __forceinline__ void mzh_run_jobs(const MzhJob* jobs, int KB, const f
 struct MzhChunk {
   const float4* w[4];
   const float* bias[4];  // already offset to the tile's first column
-  float* out;            // LDS output base
+  float* out[4];         // LDS output base per tile (a chunk may span two layers sharing A)
   int col0[4];
   int ldo, nj;           // nj: active tiles (wave-uniform), <= NJ
 };
 
 __device__ __forceinline__ MzhChunk mzh_chunk(const MzhLayer& L, int nt0, int nj, float* out, int ldo) {
   MzhChunk c;
-  c.out = out;
   c.ldo = ldo;
   c.nj = nj;
 #pragma unroll
@@ -334,6 +355,7 @@ __device__ __forceinline__ MzhChunk mzh_chunk(const MzhLayer& L, int nt0, int nj
     c.w[q] = L.w + (size_t)nt * L.kb * 64;
     c.bias[q] = L.b + nt * 16;
     c.col0[q] = nt * 16;
+    c.out[q] = out;
   }
   return c;
 }
@@ -397,7 +419,7 @@ __device__ __forceinline__ void mzh_mma_store(const floatx4* f, const float* bv,
           if (ohv) v = v + ohv[(q * MT + m) * 4 + i];  // one-hot action column (k = 64 + a)
           v = v + bv[q];
           if (relu) v = v > 0.0f ? v : 0.0f;
-          c.out[row * c.ldo + col] = v;
+          c.out[q][row * c.ldo + col] = v;
         }
       }
     }
@@ -555,6 +577,27 @@ __device__ __forceinline__ MzhChunk mzh_head_chunk(MlpSmem<R>& sm, const MzhNet&
   return mzh_chunk(net.val2, wave - 1 < net.val2.nt ? wave - 1 : 0, wave - 1 < net.val2.nt ? 1 : 0, sm.lval, MZH_LDSUP);
 }
 
+// nj consecutive tiles of the prediction hidden layers' 32-tile strip (tiles 0-15: pol0 -> hidP,
+// 16-31: val0 -> hidV; both read the normalised latent), starting at strip tile t0
+template <int R>
+__device__ __forceinline__ MzhChunk mzh_pred_tiles(MlpSmem<R>& sm, const MzhNet& net, int t0, int nj) {
+  MzhChunk c;
+  c.ldo = MZH_LD256;
+  c.nj = nj;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int t = t0 + (q < nj ? q : 0);
+    const bool v = t >= 16;
+    const MzhLayer& L = v ? net.val0 : net.pol0;
+    const int nt = t & 15;
+    c.w[q] = L.w + (size_t)nt * L.kb * 64;
+    c.bias[q] = L.b + nt * 16;
+    c.col0[q] = nt * 16;
+    c.out[q] = v ? sm.hidV : sm.hidP;
+  }
+  return c;
+}
+
 // initial_inference (networks.py:71-94): sm.x holds obs rows zero-padded to 16*rep0.kb.
 template <int R>
 __device__ void mzh_mlp_initial(MlpSmem<R>& sm, const MzhNet& net, int wave_in, int lane) {
@@ -585,7 +628,7 @@ __device__ void mzh_mlp_initial(MlpSmem<R>& sm, const MzhNet& net, int wave_in, 
   mzh_fetch<1, 16>(fa, ba, c7, lane);
   mzh_mma_store<MT, 4, 4, true>(fb, bb, c6, sm.x, MZH_LD64, true, nullptr, lane);
   __syncthreads();
-  mzh_mma_store<MT, 1, 16>(fa, ba, c7, c7.out == sm.lpol ? sm.hidP : sm.hidV, MZH_LD256, false, nullptr, lane);
+  mzh_mma_store<MT, 1, 16>(fa, ba, c7, c7.out[0] == sm.lpol ? sm.hidP : sm.hidV, MZH_LD256, false, nullptr, lane);
   __syncthreads();
   mzh_heads_par<R>(sm, sm.hidR, net.support, false, tid);
   __syncthreads();
@@ -636,8 +679,17 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(MlpSmem<R>& sm, const Mzh
                                  nullptr, lane);  // dyn2 -> h'
   MZH_STAMP(3);
   __syncthreads();
-  const bool has_r2 = wave < net.rwd2.nt;
-  mzh_fetch<1, 16>(fb, bb, mzh_chunk(net.rwd2, has_r2 ? wave : 0, has_r2 ? 1 : 0, sm.lrwd, MZH_LDSUP), lane);
+  // Phase B (after rwd0) balances rwd2 against the prediction hidden layers: with n2 = rwd2 tiles
+  // (3 for support 33), waves w < n2 run one rwd2 tile (K = 256, 4 units) + n2 + 4 prediction
+  // tiles (K = 64, 1 unit each), the others n2 + 8 prediction tiles -- 8 + n2 units per wave.
+  const int n2 = net.rwd2.nt;
+  const bool r2 = wave < n2;
+  const int P1 = r2 ? wave * (n2 + 4) : n2 * (n2 + 4) + (wave - n2) * (n2 + 8);
+  const int P2 = P1 + (r2 ? 0 : 4), P3 = P2 + 4;
+  if (r2)
+    mzh_fetch<1, 16>(fb, bb, mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP), lane);
+  else
+    mzh_fetch<4, 4, true>(fb, bb, mzh_pred_tiles<R>(sm, net, P1, 4), lane);
   MZH_STAMP(4);
   mzh_normalize_par<R>(sm.hraw, sm.x, tid);
   MZH_STAMP(5);
@@ -645,15 +697,18 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(MlpSmem<R>& sm, const Mzh
                           nullptr, lane);  // rwd0 on h' (networks.py:132)
   MZH_STAMP(6);
   __syncthreads();
-  mzh_fetch<4, 4, true>(fa, ba, mzh_pred_chunk<R>(sm, net, wave, 0), lane);
+  mzh_fetch<4, 4, true>(fa, ba, mzh_pred_tiles<R>(sm, net, P2, 4), lane);
   MZH_STAMP(7);
-  mzh_mma_store<MT, 1, 16>(fb, bb, mzh_chunk(net.rwd2, has_r2 ? wave : 0, has_r2 ? 1 : 0, sm.lrwd, MZH_LDSUP),
-                           sm.hidR, MZH_LD256, false, nullptr, lane);  // rwd2 -> reward logits
-  mzh_fetch<4, 4, true>(fb, bb, mzh_pred_chunk<R>(sm, net, wave, 1), lane);
+  if (r2)
+    mzh_mma_store<MT, 1, 16>(fb, bb, mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP), sm.hidR, MZH_LD256, false,
+                             nullptr, lane);  // rwd2 -> reward logits
+  else
+    mzh_mma_store<MT, 4, 4, true>(fb, bb, mzh_pred_tiles<R>(sm, net, P1, 4), sm.x, MZH_LD64, true, nullptr, lane);
+  mzh_fetch<3, 4>(fb, bb, mzh_pred_tiles<R>(sm, net, P3, n2), lane);
   MZH_STAMP(8);
-  mzh_mma_store<MT, 4, 4, true>(fa, ba, mzh_pred_chunk<R>(sm, net, wave, 0), sm.x, MZH_LD64, true, nullptr, lane);
+  mzh_mma_store<MT, 4, 4, true>(fa, ba, mzh_pred_tiles<R>(sm, net, P2, 4), sm.x, MZH_LD64, true, nullptr, lane);
   mzh_fetch<1, 16>(fa, ba, mzh_head_chunk<R>(sm, net, wave), lane);
-  mzh_mma_store<MT, 4, 4, true>(fb, bb, mzh_pred_chunk<R>(sm, net, wave, 1), sm.x, MZH_LD64, true, nullptr, lane);
+  mzh_mma_store<MT, 3, 4>(fb, bb, mzh_pred_tiles<R>(sm, net, P3, n2), sm.x, MZH_LD64, true, nullptr, lane);
   MZH_STAMP(9);
   __syncthreads();
   mzh_mma_store<MT, 1, 16>(fa, ba, mzh_head_chunk<R>(sm, net, wave), wave == 0 ? sm.hidP : sm.hidV, MZH_LD256,

@@ -30,6 +30,15 @@ struct __align__(128) MzhBlock {
 static_assert(sizeof(MzhBlock) == 128, "block layout");
 static_assert(__builtin_offsetof(MzhBlock, W) == 72, "block layout");
 
+// select-phase options (A/B-able in diagnostic builds): child-block prefetch one level ahead
+#ifndef MZH_SELECT_PF
+#define MZH_SELECT_PF 1
+#endif
+// next-level (N | X) word: 1 = cross-lane shuffle (measured faster), 0 = picked from the six words every lane loads
+#ifndef MZH_NX_SHFL
+#define MZH_NX_SHFL 1
+#endif
+
 // the root's 6 children live in LDS for the whole search (every simulation starts there)
 struct MzhRootBlk {
   double W[8];
@@ -54,7 +63,7 @@ struct SearchSmem {
   MzhPathEnt pc[R][DC];
   double bval[R][DC];  // value added at each cached path depth (backup value chain)
   double rootW[R];
-  double mm[R][2];  // MinMaxStats (maximum, minimum)
+  double mm[R][4];  // MinMaxStats (maximum, minimum) + normaliser (max - min, RN(1/(max - min)))
   int rootN[R];
   int firstTie[R];
   int extra[R];
@@ -93,21 +102,28 @@ __device__ __forceinline__ float mzh_ucb(int Nc, double Wc, float Rc, double P64
   return q32 + u32;
 }
 
+// MinMaxStats update with the select-side normaliser precomputed (den, RN(1/den))
+__device__ __forceinline__ void mzh_mm_set(double* mm, double mx, double mn) {
+  mm[0] = mx;
+  mm[1] = mn;
+  mm[2] = mx - mn;
+  mm[3] = mx > mn ? 1.0 / (mx - mn) : 0.0;
+}
+
 // argmax over the 6 children held by the 8-lane group, with the reference's tie handling:
 // np.random.choice(argmax set) -- the first 6-way tie takes the host-drawn index, any other tie
-// is counted (RNG-stream divergence) and resolved to the lowest index.
+// is counted (RNG-stream divergence) and resolved to the lowest index.  Branch-free; every lane
+// of the group returns the same pick.
 __device__ __forceinline__ int mzh_group_pick(float ucb, int c, int lane, int tie, int& firstTie, int& extra) {
   const float m = mzh_max8(ucb);
   const unsigned long long bal = __ballot(c < MZH_A && ucb == m);
   const unsigned mask = (unsigned)(bal >> (lane & ~7)) & 0x3Fu;
   const int cnt = __popc(mask);
-  if (cnt == 1) return __ffs(mask) - 1;
-  if (!firstTie && cnt == MZH_A) {
-    firstTie = 1;
-    return tie;
-  }
-  extra += 1;
-  return __ffs(mask) - 1;
+  const int first = __ffs(mask) - 1;
+  const bool six = (cnt == MZH_A) & (firstTie == 0);
+  extra += ((cnt > 1) & !six) ? 1 : 0;
+  firstTie |= six ? 1 : 0;
+  return six ? tie : first;
 }
 
 // x ** e with numpy semantics for the exponents generate_play_policy can produce
@@ -158,11 +174,9 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
     st.steps[r] = 0;
     st.depth[r] = 0;
     if (p.minmax_in && r < nvalid) {
-      st.mm[r][0] = p.minmax_in[2 * (root0 + r)];
-      st.mm[r][1] = p.minmax_in[2 * (root0 + r) + 1];
+      mzh_mm_set(st.mm[r], p.minmax_in[2 * (root0 + r)], p.minmax_in[2 * (root0 + r) + 1]);
     } else {
-      st.mm[r][0] = -__builtin_inf();
-      st.mm[r][1] = __builtin_inf();
+      mzh_mm_set(st.mm[r], -__builtin_inf(), __builtin_inf());
     }
   }
 
@@ -215,10 +229,8 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
       const int r = tid >> 3, c = tid & 7;
       if (r < nvalid) {
         const MzhBlock* tb = reinterpret_cast<const MzhBlock*>(p.tree) + (size_t)(root0 + r) * p.E;
-        const double mmax = st.mm[r][0], mmin = st.mm[r][1];
+        const double mmax = st.mm[r][0], mmin = st.mm[r][1], den = st.mm[r][2], dinv = st.mm[r][3];
         const bool has = mmax > mmin;
-        const double den = mmax - mmin;
-        const double dinv = has ? 1.0 / den : 0.0;
         int firstTie = st.firstTie[r];
         int extra = st.extra[r];
         const int tie = p.tie_idx ? p.tie_idx[root0 + r] : 0;
@@ -246,16 +258,25 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
         // them): the block's cache lines are in flight while this level's UCB/argmax completes
         // (unconditional loads -- a lane without a child re-reads a valid block -- so the
         // compiler can count outstanding loads and wait only for the ones a level needs)
-        int pf0 = *reinterpret_cast<const int*>(tb + (Xc >= 0 ? Xc : 0));
+        int pf0 = 0;
+        if (MZH_SELECT_PF) pf0 = *reinterpret_cast<const int*>(tb + (Xc >= 0 ? Xc : 0));
         int nx = __shfl((Nc & 0xFFFF) | (Xc << 16), (lane & ~7) + pick);
         int depth = 1, e = 0;
+
         // deeper levels: tree blocks in HBM (L2); lanes 6, 7 re-read slot 5 and act as
         // unexpanded, unvisited pads (N = 0, X = -1)
         const int cs = c < MZH_A ? c : MZH_A - 1;
+        MZH_STAMP(29);
+        MZH_LSTAMP_DECL
         while ((nx >> 16) >= 0) {
+          MZH_LSTAMP_COUNT();
           e = nx >> 16;
           const int Np = nx & 0xFFFF;
           const MzhBlock* b = tb + e;
+          // all six (N | X << 16) words (same cache line): the next level's block index is
+          // picked from registers instead of a cross-lane shuffle
+          const int4 n03 = *reinterpret_cast<const int4*>(&b->nx[0]);
+          const int2 n45 = *reinterpret_cast<const int2*>(&b->nx[4]);
           int nxc = *reinterpret_cast<const int*>(&b->nx[cs]);
           Rc = b->R[cs];
           Wc = b->W[cs];
@@ -263,21 +284,30 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
           if (c >= MZH_A) nxc = (int)0xFFFF0000;
           // retire the previous level's prefetch (older than this level's block loads, so no
           // extra wait) -- keeps it in flight inside the loop
-          asm volatile("" ::"v"(pf0));
+          if (MZH_SELECT_PF) asm volatile("" ::"v"(pf0));
           const int xc = nxc >> 16;
-          pf0 = *reinterpret_cast<const int*>(tb + (xc >= 0 ? xc : e));
+          if (MZH_SELECT_PF) pf0 = *reinterpret_cast<const int*>(tb + (xc >= 0 ? xc : e));
           Nc = nxc & 0xFFFF;
+          MZH_LSTAMP(0);
           ucb = c < MZH_A ? mzh_ucb(Nc, Wc, Rc, (double)Pc, p.np1, table[Np], disc, has, mmin, den, dinv, inv)
                           : -__builtin_inff();
+          MZH_LSTAMP(1);
           pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
+          MZH_LSTAMP(2);
           if (c == pick) {
             path[r * PL + depth] = (uint16_t)(e * 8 + pick);
             if (depth < DC) st.pc[r][depth] = MzhPathEnt{Wc, Rc, Nc};
           }
-          nx = __shfl(nxc, (lane & ~7) + pick);
+          if (MZH_NX_SHFL)
+            nx = __shfl(nxc, (lane & ~7) + pick);
+          else
+            nx = pick == 0 ? n03.x : pick == 1 ? n03.y : pick == 2 ? n03.z : pick == 3 ? n03.w : pick == 4 ? n45.x : n45.y;
           depth++;
+          MZH_LSTAMP(3);
         }
-        asm volatile("" ::"v"(pf0));
+        MZH_LSTAMP_FLUSH(24);
+        MZH_STAMP(30);
+        if (MZH_SELECT_PF) asm volatile("" ::"v"(pf0));
         if (c == 0) {
           st.depth[r] = depth;
           st.leafE[r] = e;
@@ -288,11 +318,15 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
         }
         if (!REPLAY) {
           // MLP input for this root: the parent's latent (mcts.py:89-92) and the leaf's move
-          const floatx4* hsrc = reinterpret_cast<const floatx4*>(p.htree) + ((size_t)(root0 + r) * p.E + e) * 16 + c * 2;
-          const floatx4 h0 = hsrc[0], h1 = hsrc[1];
-          float* d = &sm.x[r * MZH_LD64 + c * 8];
-          d[0] = h0[0]; d[1] = h0[1]; d[2] = h0[2]; d[3] = h0[3];
-          d[4] = h1[0]; d[5] = h1[1]; d[6] = h1[2]; d[7] = h1[3];
+          // MLP input: the leaf's parent latent (mcts.py:89-92).  The node expanded by the previous
+          // simulation (index s; the root at s = 0) is still in sm.x as that MLP's output.
+          if (e != s) {
+            const floatx4* hsrc = reinterpret_cast<const floatx4*>(p.htree) + ((size_t)(root0 + r) * p.E + e) * 16 + c * 2;
+            const floatx4 h0 = hsrc[0], h1 = hsrc[1];
+            float* d = &sm.x[r * MZH_LD64 + c * 8];
+            d[0] = h0[0]; d[1] = h0[1]; d[2] = h0[2]; d[3] = h0[3];
+            d[4] = h1[0]; d[5] = h1[1]; d[6] = h1[2]; d[7] = h1[3];
+          }
           if (c == 0) sm.act[r] = pick;
         }
       }
@@ -416,8 +450,7 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kerne
         mzh_maxmin8d(lmax, lmin);
         if (c == 0) {
           const double mx = st.mm[r][0], mn = st.mm[r][1];
-          st.mm[r][0] = lmax > mx ? lmax : mx;
-          st.mm[r][1] = lmin < mn ? lmin : mn;
+          mzh_mm_set(st.mm[r], lmax > mx ? lmax : mx, lmin < mn ? lmin : mn);
         }
       }
     }

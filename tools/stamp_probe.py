@@ -7,7 +7,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["MZH_LIB"] = os.path.join(ROOT, "muzero-hanoi_amd", "libmzh_diag.so")
+os.environ["MZH_LIB"] = os.environ.get("MZH_DIAG_LIB", os.path.join(ROOT, "muzero-hanoi_amd", "libmzh_diag.so"))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -16,8 +16,8 @@ from muzero_hanoi_amd import _lib, engine, rng  # noqa: E402
 from muzero_hanoi_amd.networks import MuZeroNet  # noqa: E402
 
 MLP = {0: "prologue", 1: "dyn0", 2: "bar+fetch", 3: "dyn2", 4: "bar+fetch", 5: "norm", 6: "rwd0", 7: "bar+fetch",
-       8: "rwd2+fetch", 9: "pol0/val0 x2", 10: "bar+pol2/val2", 11: "bar+heads", 12: "bar"}
-SEARCH = {16: "loop-top", 17: "select", 18: "bar", 19: "gather+bar", 20: "mlp", 21: "store h", 22: "expand+backup",
+       8: "rwd2|pred4", 9: "pred4+pred3", 10: "bar+pol2/val2", 11: "bar+heads", 12: "bar"}
+SEARCH = {16: "loop-top", 29: "select:root level", 30: "select:loop", 17: "select:gather", 18: "bar", 19: "gather+bar", 20: "mlp", 21: "store h", 22: "expand+backup",
           23: "bar"}
 
 
@@ -30,7 +30,7 @@ def main():
     eng.load_weights(engine.flat_weights(net.state_dict()))
     L = _lib.lib()
     L.mzh_diag_stamps.argtypes = [ctypes.c_void_p]
-    buf = np.zeros((8, 24), np.uint64)
+    buf = np.zeros((8, 32), np.uint64)
     h = torch.rand((B, 64), device="cuda")
     a = torch.randint(0, 6, (B,), dtype=torch.int32, device="cuda")
     eng.recurrent_inference(h, a)
@@ -53,9 +53,13 @@ def main():
     eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u)
     torch.cuda.synchronize()
     L.mzh_diag_stamps(buf.ctypes.data)
-    per = (buf / S).astype(np.int64)
+    per = buf / S
     out["search_per_sim"] = {f"{k}:{v}": per[:4, k].tolist() for k, v in SEARCH.items()}
-    out["search_per_sim_total"] = per[:4, 16:24].sum(1).tolist()
+    out["search_per_sim_total"] = (per[:4, 16:24].sum(1) + per[:4, 29] + per[:4, 30]).tolist()
+    lv = {24: "mem(block)", 25: "ucb", 26: "pick", 27: "path+shfl"}
+    its = per[:4, 28] * S
+    out["select_level_ticks"] = {f"{k}:{v}": (per[:4, k] * S / np.maximum(its, 1)).round().tolist() for k, v in lv.items()}
+    out["select_levels_per_sim"] = (its / S).tolist()
     out["mlp_in_search_per_sim"] = {f"{k}:{v}": per[:4, k].tolist() for k, v in MLP.items()}
     print(json.dumps(out, indent=1))
 
