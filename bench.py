@@ -47,6 +47,7 @@ def parse():
     p.add_argument("--disks", type=int, default=4)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-gather", action="store_true")
+    p.add_argument("--kernel", choices=["auto", "coop", "wave"], default="auto")
     p.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
@@ -124,11 +125,12 @@ def main():
     noise, tie, u = (torch.from_numpy(sl(x)).to(dev) for x in (noise, tie, u))
     out = eng.alloc_search_outputs(B, S)
     gather = dist is not None and not a.no_gather
+    kern = None if a.kernel == "auto" else a.kernel
     stream = torch.cuda.current_stream(dev)
 
     def step():
         eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, temperature=1.0, deterministic=False,
-                   discount=0.8, eps=0.25, out=out)
+                   discount=0.8, eps=0.25, out=out, kernel=kern)
         if gather:
             return mdist.gather_visits(out["visits"], GB, world)
 
@@ -149,7 +151,7 @@ def main():
     for k in range(a.steps):
         evs[k][0].record(stream)
         eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, temperature=1.0, deterministic=False,
-                   discount=0.8, eps=0.25, out=out)
+                   discount=0.8, eps=0.25, out=out, kernel=kern)
         evs[k][1].record(stream)
         if gather:
             mdist.gather_visits(out["visits"], GB, world)

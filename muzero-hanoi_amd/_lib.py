@@ -20,6 +20,8 @@ MZH_ERR_CAPACITY = -3
 MZH_ERR_STATE = -4
 MZH_ERR_TEMPERATURE = -5
 MZH_FLAG_NP1_UCB = 1
+MZH_FLAG_KERNEL_COOP = 2  # cooperative kernel (mzh_search.hip)
+MZH_FLAG_KERNEL_WAVE = 4  # wave-independent kernel (mzh_wave.hip)
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32

@@ -56,8 +56,10 @@ struct mzh_engine {
   void* wbuf = nullptr;
   bool loaded = false;
   MzhNet net{};
+  MzhWNet wnet{};
   unsigned char* tree = nullptr;
   float* htree = nullptr;
+  uint16_t* pathx = nullptr;
   double* table = nullptr;
 };
 
@@ -116,6 +118,7 @@ extern "C" int mzh_create(int device, int n_disks, int max_sims, int max_roots, 
   const size_t nblk = (size_t)max_roots * eng->E;
   hipError_t e = hipMalloc(&eng->tree, nblk * 128)  /* MzhBlock: one cache line */;
   if (e == hipSuccess) e = hipMalloc(&eng->htree, nblk * MZH_LATENT * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&eng->pathx, nblk * sizeof(uint16_t));
   if (e == hipSuccess) e = hipMalloc(&eng->table, sizeof(double) * (size_t)(max_sims + 2));
   if (e != hipSuccess) {
     mzh_destroy(eng);
@@ -138,6 +141,7 @@ extern "C" int mzh_destroy(mzh_engine* eng) {
   DeviceGuard g(eng->device);
   if (eng->tree) (void)hipFree(eng->tree);
   if (eng->htree) (void)hipFree(eng->htree);
+  if (eng->pathx) (void)hipFree(eng->pathx);
   if (eng->table) (void)hipFree(eng->table);
   if (eng->wbuf) (void)hipFree(eng->wbuf);
   delete eng;
@@ -173,6 +177,63 @@ static PackedLayer pack_layer(std::vector<float>& buf, const float* W, const flo
   return L;
 }
 
+// ---- wave-kernel packing (MzhWMlp, mzh_internal.h): weights as the MFMA A operand ----
+static int wperm_u(int ht, int r) { return 16 * ht + 4 * (r & 3) + (r >> 2); }
+enum WOut { WOUT_LATENT, WOUT_HEAD33, WOUT_NATURAL };
+// output unit held by C row r (= 4g + i) of output tile ot, -1 for a padding row
+static int wperm_out(WOut kind, int ot, int r, int n_out) {
+  if (kind == WOUT_LATENT) return wperm_u(ot, r);
+  if (kind == WOUT_HEAD33) {
+    const int g = r >> 2, i = r & 3, sl = 4 * ot + i;
+    const int k = 2 * g + (sl & 1) + 8 * (sl >> 1);  // partial q = 2g + (sl & 1), term sl >> 1
+    return k < n_out ? k : -1;
+  }
+  const int k = 16 * ot + r;
+  return k < n_out ? k : -1;
+}
+struct PackedW {
+  size_t soff = 0, b1off = 0, b2off = 0;
+  int kb1 = 0, no = 0;
+};
+static PackedW pack_wmlp(std::vector<float>& buf, const float* W1, const float* b1, int K1, int ldw1, const float* W2,
+                         const float* b2, int n_out, WOut kind) {
+  PackedW P;
+  P.kb1 = (K1 + 15) / 16;
+  P.no = (n_out + 15) / 16;
+  const int FR = P.kb1 + P.no;
+  while (buf.size() % 4) buf.push_back(0.0f);
+  P.soff = buf.size();
+  buf.resize(buf.size() + (size_t)17 * FR * 64 * 4, 0.0f);  // ht block 16 = zero pad
+  float* s = buf.data() + P.soff;
+  for (int ht = 0; ht < 16; ++ht)
+    for (int lane = 0; lane < 64; ++lane)
+      for (int t = 0; t < 4; ++t) {
+        const int r = lane & 15, gk = lane >> 4;
+        for (int kb = 0; kb < P.kb1; ++kb) {
+          const int k = 16 * kb + 4 * t + gk;
+          s[(((size_t)ht * FR + kb) * 64 + lane) * 4 + t] = k < K1 ? W1[(size_t)wperm_u(ht, r) * ldw1 + k] : 0.0f;
+        }
+        for (int ot = 0; ot < P.no; ++ot) {
+          const int row = wperm_out(kind, ot, r, n_out);
+          const int k = 16 * ht + 4 * t + gk;
+          s[(((size_t)ht * FR + P.kb1 + ot) * 64 + lane) * 4 + t] = row >= 0 ? W2[(size_t)row * MZH_HIDDEN + k] : 0.0f;
+        }
+      }
+  P.b1off = buf.size();
+  buf.resize(buf.size() + MZH_HIDDEN, 0.0f);
+  for (int ht = 0; ht < 16; ++ht)
+    for (int r = 0; r < 16; ++r) buf[P.b1off + 16 * ht + r] = b1[wperm_u(ht, r)];
+  P.b2off = buf.size();
+  buf.resize(buf.size() + (size_t)16 * P.no, 0.0f);
+  for (int ot = 0; ot < P.no; ++ot)
+    for (int r = 0; r < 16; ++r) {
+      const int row = wperm_out(kind, ot, r, n_out);
+      buf[P.b2off + 16 * ot + r] = row >= 0 ? b2[row] : 0.0f;
+    }
+  while (buf.size() % 4) buf.push_back(0.0f);
+  return P;
+}
+
 extern "C" int mzh_load_weights(mzh_engine* eng, const float* flat, size_t n_floats) {
   if (!eng || !flat) return fail(MZH_ERR_ARG, "engine or weights NULL");
   const size_t want = canonical_size(eng->in_dim, eng->support);
@@ -204,6 +265,18 @@ extern "C" int mzh_load_weights(mzh_engine* eng, const float* flat, size_t n_flo
   buf.resize(buf.size() + (size_t)A * F);
   for (int a = 0; a < A; ++a)
     for (int n = 0; n < F; ++n) buf[ohoff + (size_t)a * F + n] = dyn0w[(size_t)n * (H + A) + H + a];
+  // wave-kernel layout
+  const WOut vkind = sup == 33 ? WOUT_HEAD33 : WOUT_NATURAL;
+  PackedW WL[5];
+  WL[0] = pack_wmlp(buf, rep0w, rep0b, in, in, rep2w, rep2b, H, WOUT_LATENT);
+  WL[1] = pack_wmlp(buf, dyn0w, dyn0b, H, H + A, dyn2w, dyn2b, H, WOUT_LATENT);
+  WL[2] = pack_wmlp(buf, rwd0w, rwd0b, H, H, rwd2w, rwd2b, sup, vkind);
+  WL[3] = pack_wmlp(buf, pol0w, pol0b, H, H, pol2w, pol2b, A, WOUT_NATURAL);
+  WL[4] = pack_wmlp(buf, val0w, val0b, H, H, val2w, val2b, sup, vkind);
+  const size_t wohoff = buf.size();
+  buf.resize(buf.size() + (size_t)A * F, 0.0f);
+  for (int a = 0; a < A; ++a)
+    for (int j = 0; j < F; ++j) buf[wohoff + (size_t)a * F + j] = dyn0w[(size_t)wperm_u(j >> 4, j & 15) * (H + A) + H + a];
 
   DeviceGuard g(eng->device);
   if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
@@ -230,6 +303,20 @@ extern "C" int mzh_load_weights(mzh_engine* eng, const float* flat, size_t n_flo
   n.dyn0_onehot = base + ohoff;
   n.support = sup;
   n.in_dim = in;
+  auto mkw = [&](const PackedW& pw) {
+    MzhWMlp m;
+    m.s = reinterpret_cast<const float4*>(base + pw.soff);
+    m.b1 = base + pw.b1off;
+    m.b2 = base + pw.b2off;
+    m.kb1 = pw.kb1;
+    m.no = pw.no;
+    return m;
+  };
+  MzhWNet& w = eng->wnet;
+  w.rep = mkw(WL[0]); w.dyn = mkw(WL[1]); w.rwd = mkw(WL[2]); w.pol = mkw(WL[3]); w.val = mkw(WL[4]);
+  w.oh = base + wohoff;
+  w.support = sup;
+  w.in_dim = in;
   eng->loaded = true;
   return MZH_OK;
 }
@@ -317,6 +404,22 @@ extern "C" int mzh_recurrent_inference(mzh_engine* eng, int B, const float* h_in
 // ---- search ----
 static const size_t kMaxLds = 163840;
 
+// kernel choice: the wave-independent kernel (mzh_wave.hip) needs >= 2 waves of 32 roots per SIMD
+// to overlap its tree and MFMA phases; smaller batches run the cooperative kernel (mzh_search.hip)
+// whose 4 waves share one 32-root MLP tile.  MZH_FLAG_KERNEL_* (or MZH_KERNEL=coop|wave) force one.
+static const int kWaveMinRoots = 32768;
+static bool use_wave_kernel(int B, uint32_t flags) {
+  if (flags & MZH_FLAG_KERNEL_WAVE) return true;
+  if (flags & MZH_FLAG_KERNEL_COOP) return false;
+  static const int forced = [] {
+    const char* v = getenv("MZH_KERNEL");
+    if (!v) return 0;
+    return strcmp(v, "wave") == 0 ? 1 : strcmp(v, "coop") == 0 ? -1 : 0;
+  }();
+  if (forced) return forced > 0;
+  return B >= kWaveMinRoots;
+}
+
 static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream stream, bool replay) {
   if (!eng || !a) return fail(MZH_ERR_ARG, "engine or args NULL");
   if (a->B < 0 || a->n_sims < 0) return fail(MZH_ERR_ARG, "B=%d n_sims=%d", a->B, a->n_sims);
@@ -335,10 +438,16 @@ static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream s
   }
   if (!a->deterministic && !a->action_u && a->action)
     return fail(MZH_ERR_ARG, "stochastic action selection needs action_u");
+  const bool wave = use_wave_kernel(a->B, a->flags);
   int R = pick_rows(a->B);
-  if (mzh_search_smem_bytes(R, a->n_sims) > kMaxLds) R = 16;
-  if (mzh_search_smem_bytes(R, a->n_sims) > kMaxLds)
-    return fail(MZH_ERR_CAPACITY, "n_sims=%d exceeds the LDS path budget", a->n_sims);
+  if (wave) {
+    if (mzh_wave_smem_bytes(a->n_sims) > kMaxLds)
+      return fail(MZH_ERR_CAPACITY, "n_sims=%d exceeds the wave kernel's LDS table budget", a->n_sims);
+  } else {
+    if (mzh_search_smem_bytes(R, a->n_sims) > kMaxLds) R = 16;
+    if (mzh_search_smem_bytes(R, a->n_sims) > kMaxLds)
+      return fail(MZH_ERR_CAPACITY, "n_sims=%d exceeds the LDS path budget", a->n_sims);
+  }
   DeviceGuard g(eng->device);
   if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
   MzhSearchParams p{};
@@ -347,10 +456,11 @@ static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream s
   p.discount = a->discount; p.eps = a->eps; p.temperature = a->temperature;
   p.obs = a->obs; p.noise = a->noise; p.tie_idx = a->tie_idx; p.action_u = a->action_u; p.minmax_in = a->minmax_in;
   p.rp_root_pi = a->rp_root_pi; p.rp_pi = a->rp_pi; p.rp_reward = a->rp_reward; p.rp_value = a->rp_value;
-  p.tree = eng->tree; p.htree = eng->htree; p.table = eng->table;
+  p.tree = eng->tree; p.htree = eng->htree; p.pathx = eng->pathx; p.table = eng->table;
   p.visits = a->visits; p.root_q = a->root_q; p.minmax_out = a->minmax_out; p.extra_ties = a->extra_ties;
   p.action = a->action; p.pi = a->pi; p.latent = a->latent; p.latent_len = a->latent_len; p.sel_steps = a->sel_steps;
-  hipError_t e = mzh_launch_search(R, replay, eng->net, p, (hipStream_t)stream);
+  hipError_t e = wave ? mzh_launch_wave_search(replay, eng->wnet, p, (hipStream_t)stream)
+                      : mzh_launch_search(R, replay, eng->net, p, (hipStream_t)stream);
   return e == hipSuccess ? MZH_OK : hip_fail(e, "search launch");
 }
 

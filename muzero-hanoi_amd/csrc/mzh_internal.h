@@ -22,6 +22,7 @@ struct MzhSearchParams {
   const float* rp_value;
   unsigned char* tree;  // [B][E] MzhBlock
   float* htree;         // [B][E][64]
+  uint16_t* pathx;      // [B][E] selection-path slots beyond the LDS-cached depths (wave kernel)
   const double* table;  // [S+2] UCB table (log((n+19653)/19652)+1.25)*sqrt(n)
   int32_t* visits;
   double* root_q;
@@ -75,6 +76,33 @@ __device__ __forceinline__ void mzh_store_outputs(MlpSmem<R>& sm, const MzhInfer
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Wave-kernel network layout (mzh_wave.hip).  Each MLP (layer1 -> ReLU -> layer2) is one stream
+// of MFMA A-fragments with the WEIGHTS as the A operand and the activations (one root per
+// column) as the B operand, so a hidden tile's C registers feed the next layer's B operand
+// directly (no LDS round trip).  Per hidden tile ht (16 units) the stream holds KB1 layer-1
+// fragments then NO layer-2 fragments, each [64 lanes] float4:
+//   layer1 frag (ht, kb)[lane][t] = W1[u(ht, lane&15)][16kb + 4t + (lane>>4)]
+//   layer2 frag (ht, ot)[lane][t] = W2[pi(ot, lane&15)][16ht + 4t + (lane>>4)]
+// with u(ht, r) = 16ht + 4(r&3) + (r>>2): C row 4g+i of hidden tile ht is unit 16ht + 4i + g, which
+// is exactly the unit lane group g must supply at k-step i of layer 2 -- every dot product stays
+// a k-ordered fp32 FMA chain from 0 (the numerics contract of mzh_device.h).  One zero ht block
+// pads the stream end (unconditional prefetch).  b1/b2 are the biases in C-register order.
+// ------------------------------------------------------------------------------------------
+struct MzhWMlp {
+  const float4* s;  // [17][KB1 + NO][64]
+  const float* b1;  // [256]: b1[16ht + 4g + i] = bias1[16ht + 4i + g]
+  const float* b2;  // [16 NO]: b2[16ot + 4g + i] = bias2[pi(ot, 4g + i)] (0 on padding rows)
+  int kb1, no;
+};
+struct MzhWNet {
+  MzhWMlp rep, dyn, rwd, pol, val;
+  const float* oh;  // [6][256]: oh[a][16ht + 4g + i] = dynamic_net.0.weight[u(ht, 4g + i)][64 + a]
+  int support, in_dim;
+};
+
+size_t mzh_wave_smem_bytes(int S);
+hipError_t mzh_launch_wave_search(bool replay, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream);
 size_t mzh_search_smem_bytes(int R, int S);
 hipError_t mzh_launch_search(int R, bool replay, const MzhNet& net, const MzhSearchParams& p, hipStream_t stream);
 hipError_t mzh_launch_infer(int R, bool recurrent, const MzhNet& net, const MzhInferParams& p, hipStream_t stream);

@@ -143,7 +143,10 @@ def test_mlp_batch_sizes_vs_oracle(mzh, oracle, B):
 
 
 # ------------------------------------------------------------------------------------ search
-def _run_replay_case(mzh, g):
+KERNELS = ["coop", "wave"]
+
+
+def _run_replay_case(mzh, g, kernel=None):
     S, n = int(g["s"]), int(g["n"])
     det, T = bool(g["deterministic"]), float(g["temperature"])
     rp = replay_inputs(g)
@@ -158,21 +161,22 @@ def _run_replay_case(mzh, g):
             noise, tie, u = draws[b]
             o = eng.search(S, replay={k: tt(v[b:b + 1]) for k, v in dict(root_pi=rp["root_pi"], pi=rp["pi"], reward=rp["rwd"], value=rp["value"]).items()},
                            tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), minmax_in=mm,
-                           temperature=T, deterministic=det, discount=float(g["discount"]))
+                           temperature=T, deterministic=det, discount=float(g["discount"]), kernel=kernel)
             mm = o["minmax"].clone()
             outs.append({k: v.cpu().numpy() for k, v in o.items() if k != "_keep"})
         return {k: np.concatenate([o[k] for o in outs]) for k in outs[0]}
     noise, tie, u = replay_draws(g)
     o = eng.search(S, replay=dict(root_pi=tt(rp["root_pi"]), pi=tt(rp["pi"]), reward=tt(rp["rwd"]), value=tt(rp["value"])),
                    tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=T, deterministic=det,
-                   discount=float(g["discount"]))
+                   discount=float(g["discount"]), kernel=kernel)
     return {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("case", REPLAY_CASES)
-def test_search_replay_bit_exact_vs_reference(mzh, case):
+def test_search_replay_bit_exact_vs_reference(mzh, case, kernel):
     g = golden(f"replay_{case}.npz")
-    out = _run_replay_case(mzh, g)
+    out = _run_replay_case(mzh, g, kernel)
     assert np.array_equal(out["visits"], g["visits"])
     assert np.array_equal(out["root_q"], g["rootQ"])
     assert np.array_equal(out["minmax"][:, 0], g["mm_max"]) and np.array_equal(out["minmax"][:, 1], g["mm_min"])
@@ -185,8 +189,9 @@ def test_search_replay_bit_exact_vs_reference(mzh, case):
         assert list(out["latent"][b][:L]) == [int(v) for v in want[want >= 0]]
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("case", [c for c in REPLAY_CASES if "shared" not in c])
-def test_search_mlp_end_to_end_vs_oracle(mzh, oracle, case):
+def test_search_mlp_end_to_end_vs_oracle(mzh, oracle, case, kernel):
     """Full fused search (MLP on MFMA) == oracle search with the same weights, bit for bit."""
     g = golden(f"replay_{case}.npz")
     S, n, td = int(g["s"]), int(g["n"]), int(g["td"])
@@ -197,7 +202,7 @@ def test_search_mlp_end_to_end_vs_oracle(mzh, oracle, case):
     eng = _engine(mzh, n, S, B, sup, flat)
     tt = lambda a: None if a is None else torch.tensor(np.asarray(a), device=DEV)
     o = eng.search(S, obs=tt(g["obs"].astype(np.float32)), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u),
-                   temperature=T, deterministic=det, discount=float(g["discount"]))
+                   temperature=T, deterministic=det, discount=float(g["discount"]), kernel=kernel)
     o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
     ref = oracle.search(n, S, g["obs"], flat=flat, support=sup, noise=noise, tie_idx=tie, action_u=u,
                         temperature=T, deterministic=det, discount=float(g["discount"]))
@@ -210,8 +215,9 @@ def test_search_mlp_end_to_end_vs_oracle(mzh, oracle, case):
     assert agree >= 0.5, agree
 
 
-@pytest.mark.parametrize("B,S,n", [(40, 50, 4), (700, 25, 3), (9000, 8, 4)])
-def test_search_batched_vs_oracle_random_roots(mzh, oracle, B, S, n):
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("B,S,n", [(40, 50, 4), (700, 25, 3), (9000, 8, 4), (300, 20, 7)])
+def test_search_batched_vs_oracle_random_roots(mzh, oracle, B, S, n, kernel):
     """Ragged batches (not multiples of the 16/32-root tile), both tile sizes, vs the oracle."""
     flat, in_dim, sup = _weights(oracle, f"weights_N{n}_s0")
     rs = np.random.RandomState(B + S)
@@ -223,7 +229,7 @@ def test_search_batched_vs_oracle_random_roots(mzh, oracle, B, S, n):
     noise, tie, u = rng.synthetic_draws(B, deterministic=False, alpha=0.25, seed=B)
     eng = _engine(mzh, n, S, B, sup, flat)
     tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
-    o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0)
+    o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0, kernel=kernel)
     o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
     nchk = min(B, 300)
     ref = oracle.search(n, S, obs[:nchk], flat=flat, support=sup, noise=noise[:nchk], tie_idx=tie[:nchk],
@@ -232,3 +238,69 @@ def test_search_batched_vs_oracle_random_roots(mzh, oracle, B, S, n):
     assert np.array_equal(o["root_q"][:nchk], ref["rootQ"])
     assert np.array_equal(o["action"][:nchk], ref["action"])
     assert np.all(o["visits"].sum(1) == S)
+
+
+def _random_search_inputs(B, n, seed):
+    from muzero_hanoi_amd import rng
+
+    rs = np.random.RandomState(seed)
+    st = rs.randint(0, 3, (B, n))
+    obs = np.zeros((B, 3 * n), np.float32)
+    obs[np.arange(B)[:, None], np.arange(n) * 3 + st] = 1
+    noise, tie, u = rng.synthetic_draws(B, deterministic=False, alpha=0.25, seed=seed)
+    return obs, noise, tie, u
+
+
+@pytest.mark.parametrize("B,S,n,td", [(40000, 50, 4, 1), (33000, 12, 3, 0)])
+def test_search_wave_equals_coop_large_batch(mzh, oracle, B, S, n, td):
+    """At the bench's batch sizes the two kernels agree on every output, bit for bit (ragged last
+    workgroup included), and a sample of roots matches the oracle."""
+    flat, in_dim, sup = _weights(oracle, f"weights_N{n}_s0{'' if td else '_mc'}")
+    obs, noise, tie, u = _random_search_inputs(B, n, B + S)
+    eng = _engine(mzh, n, S, B, sup, flat)
+    tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
+    res = {}
+    for kernel in KERNELS:
+        o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0,
+                       kernel=kernel)
+        res[kernel] = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+    for k in res["coop"]:
+        assert np.array_equal(res["coop"][k], res["wave"][k], equal_nan=True), k
+    idx = np.r_[0:32, B - 40:B]
+    ref = oracle.search(n, S, obs[idx], flat=flat, support=sup, noise=noise[idx], tie_idx=tie[idx],
+                        action_u=u[idx], temperature=1.0)
+    assert np.array_equal(res["wave"]["visits"][idx], ref["visits"])
+    assert np.array_equal(res["wave"]["root_q"][idx], ref["rootQ"])
+    assert np.array_equal(res["wave"]["sel_steps"][idx], ref["sel_steps"])
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_search_deep_paths_replay(mzh, oracle, kernel):
+    """Replayed network outputs that drive the search down one long chain (depth >> the 16 path
+    levels cached in LDS): visits, root Q, min-max and the latent path vs the oracle."""
+    B, S, n = 70, 120, 4
+    g = np.random.default_rng(7)
+    pi = np.full((B, S, 6), 0.002, np.float32)
+    pi[:, :, 0] = 0.99
+    root_pi = np.full((B, 6), 1.0 / 6, np.float32)
+    value = (5.0 + g.normal(0, 0.1, (B, S))).astype(np.float32)
+    rwd = g.normal(0, 0.01, (B, S)).astype(np.float32)
+    rp = dict(root_pi=root_pi, pi=pi, rwd=rwd, value=value)
+    obs = np.zeros((B, 3 * n), np.float32)
+    obs[:, 0::3] = 1
+    from muzero_hanoi_amd import rng
+
+    noise, tie, u = rng.synthetic_draws(B, deterministic=True, alpha=0.0, seed=3)
+    eng = _engine(mzh, n, S, B)
+    tt = lambda a: None if a is None else torch.tensor(np.asarray(a), device=DEV)
+    o = eng.search(S, replay=dict(root_pi=tt(root_pi), pi=tt(pi), reward=tt(rwd), value=tt(value)), tie_idx=tt(tie),
+                   noise=None, action_u=None, temperature=1.0, deterministic=True, kernel=kernel)
+    o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+    ref = oracle.search(n, S, obs, replay=rp, tie_idx=tie, temperature=1.0, deterministic=True)
+    assert ref["latent_len"].max() > 16  # deeper than the wave kernel's LDS path cache
+    assert np.array_equal(o["visits"], ref["visits"])
+    assert np.array_equal(o["root_q"], ref["rootQ"])
+    assert np.array_equal(o["minmax"][:, 0], ref["mm_max"]) and np.array_equal(o["minmax"][:, 1], ref["mm_min"])
+    assert np.array_equal(o["latent_len"], ref["latent_len"])
+    assert np.array_equal(o["latent"], ref["latent"])
+    assert np.array_equal(o["sel_steps"], ref["sel_steps"])
