@@ -68,7 +68,12 @@ def build(verbose=False, force=False, diag=False, tag="", defines=()):
 if __name__ == "__main__":
     # --variant tag=DEF1,DEF2 : diagnostic A/B build libmzh_diag_<tag>.so
     var = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--variant=")]
-    if var:
+    fvar = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--fast-variant=")]
+    if fvar:  # timing A/B build without stamps: libmzh_<tag>.so
+        tag, defs = fvar[0].split("=", 1) if "=" in fvar[0] else (fvar[0], "")
+        print(build(verbose=True, force="--force" in sys.argv, diag=False, tag=tag,
+                    defines=[d for d in defs.split(",") if d]))
+    elif var:
         tag, defs = var[0].split("=", 1) if "=" in var[0] else (var[0], "")
         print(build(verbose=True, force="--force" in sys.argv, diag=True, tag=tag,
                     defines=[d for d in defs.split(",") if d]))

@@ -18,10 +18,27 @@
 #include "mzh_device.h"
 #include "mzh_internal.h"
 
+#ifndef MZW_WAVES
 #define MZW_WAVES 4   // waves per workgroup (independent after the start-up barrier)
+#endif
+#ifndef MZW_STAGGER
+#define MZW_STAGGER 0  // start delay (s_sleep units of 64 cycles) of the second wave of each SIMD
+#endif
 #define MZW_NT 2      // 16-root column tiles per wave
 #define MZW_ROOTS 32  // roots per wave
 #define MZW_DC 16     // selection-path depths cached in LDS per root (deeper: HBM pathx)
+#ifndef MZW_PIN
+#define MZW_PIN 1     // pin the weight prefetch one hidden block ahead (sched_barrier)
+#endif
+#ifndef MZW_UNROLL
+#define MZW_UNROLL 2
+#endif
+#define MZW_STR(x) #x
+#define MZW_XSTR(x) MZW_STR(x)
+#define MZW_UNROLL_PRAGMA _Pragma(MZW_XSTR(unroll MZW_UNROLL))
+#ifndef MZW_FENCE
+#define MZW_FENCE 1   // 1: workgroup-scope fence at the end of each simulation, 0: wavefront scope
+#endif
 
 // tree block: identical to mzh_search.hip's MzhBlock (one 128-B line per expanded node)
 struct MzwNX {
@@ -85,19 +102,32 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[M
   constexpr int FR = KB1 + NO;
   const int g = lane >> 4;
   const floatx4* S = reinterpret_cast<const floatx4*>(L.s) + lane;
+  const float* B1 = L.b1 + 4 * g;
 #pragma unroll
   for (int ot = 0; ot < NO; ++ot)
 #pragma unroll
     for (int n = 0; n < MZW_NT; ++n) out[ot][n] = floatx4{0.f, 0.f, 0.f, 0.f};
-  floatx4 w[FR];
+  floatx4 w[FR], b, o[MZW_NT];
 #pragma unroll
   for (int f = 0; f < FR; ++f) w[f] = S[f * 64];
-#pragma unroll 2
+  b = *reinterpret_cast<const floatx4*>(B1);
+#pragma unroll
+  for (int n = 0; n < MZW_NT; ++n)
+    o[n] = OH ? *reinterpret_cast<const floatx4*>(n == 0 ? oh0 : oh1) : floatx4{0.f, 0.f, 0.f, 0.f};
+  MZW_UNROLL_PRAGMA
   for (int ht = 0; ht < 16; ++ht) {
-    floatx4 wn[FR];
+    // next block's fragments, bias and one-hot columns: issued here and kept in flight across
+    // this block's MFMAs (the scheduling barrier stops the compiler from sinking the loads to
+    // their uses, which would expose the L2 latency once per fragment)
+    floatx4 wn[FR], bn, on[MZW_NT];
 #pragma unroll
     for (int f = 0; f < FR; ++f) wn[f] = S[((ht + 1) * FR + f) * 64];  // block 16 is the zero pad
-    const floatx4 b = *reinterpret_cast<const floatx4*>(L.b1 + 16 * ht + 4 * g);
+    bn = *reinterpret_cast<const floatx4*>(B1 + 16 * ((ht + 1) & 15));
+#pragma unroll
+    for (int n = 0; n < MZW_NT; ++n)
+      on[n] = OH ? *reinterpret_cast<const floatx4*>((n == 0 ? oh0 : oh1) + 16 * ((ht + 1) & 15))
+                 : floatx4{0.f, 0.f, 0.f, 0.f};
+    if (MZW_PIN) __builtin_amdgcn_sched_barrier(0);
     floatx4 acc[MZW_NT];
 #pragma unroll
     for (int n = 0; n < MZW_NT; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -111,12 +141,10 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[M
     floatx4 hid[MZW_NT];
 #pragma unroll
     for (int n = 0; n < MZW_NT; ++n) {
-      floatx4 o = floatx4{0.f, 0.f, 0.f, 0.f};
-      if (OH) o = *reinterpret_cast<const floatx4*>((n == 0 ? oh0 : oh1) + 16 * ht);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float v = acc[n][i];
-        if (OH) v = v + o[i];  // one-hot action column (k = 64 + a)
+        if (OH) v = v + o[n][i];  // one-hot action column (k = 64 + a)
         v = v + b[i];
         hid[n][i] = v > 0.0f ? v : 0.0f;
       }
@@ -130,6 +158,9 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[M
           out[ot][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[KB1 + ot][t], hid[n][t], out[ot][n], 0, 0, 0);
 #pragma unroll
     for (int f = 0; f < FR; ++f) w[f] = wn[f];
+    b = bn;
+#pragma unroll
+    for (int n = 0; n < MZW_NT; ++n) o[n] = on[n];
   }
 }
 
@@ -306,7 +337,7 @@ __device__ __forceinline__ int mzw_pick(const float (&u)[6], int tie, int& first
 }
 
 template <bool REPLAY, bool SUP33>
-__global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net, MzhSearchParams p) {
+__global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel(MzhWNet net, MzhSearchParams p) {
   constexpr int NOV = SUP33 ? 3 : 1;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   const int S = p.S;
@@ -324,6 +355,11 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
     inv[i] = 1.0 / (double)i;  // IEEE division: correctly rounded
   }
   __syncthreads();  // the only barrier: from here on every wave runs independently
+  if (MZW_STAGGER > 0 && wave >= 4) {
+    // waves w and w + 4 share a SIMD: start the second one about a tree phase later so the two
+    // alternate between MFMA and tree work instead of running their phases in lockstep
+    for (int i = 0; i < MZW_STAGGER / 127; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   const int wr0 = (blockIdx.x * MZW_WAVES + wave) * MZW_ROOTS;
   if (wr0 >= p.B) return;
   MzwWave& ws = wsa[wave];
@@ -429,7 +465,9 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
   }
   mzw_wave_sync();
 
+  MZH_STAMP_DECL
   for (int s = 0; s < S; ++s) {
+    MZH_STAMP(0);
     // ---------------- select (mcts.py:75-86; node.py:72-123): one lane per root ----------------
     if (rvalid) {
       const bool has = mmax > mmin;
@@ -496,6 +534,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
       leafA = pick;
       steps += d;
     }
+    MZH_STAMP(1);
 
     // ---------------- expand via the network (mcts.py:88-106) ----------------
     float val[MZW_NT], rew[MZW_NT];
@@ -519,9 +558,11 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
           for (int kb = 0; kb < 4; ++kb) x[n][kb] = src[4 * kb];
         }
       }
+      MZH_STAMP(2);
       floatx4 hp[4][MZW_NT];
       mzw_chain<4, 4, true>(net.dyn, x, ohl + an[0] * MZH_F + 4 * g, ohl + an[1] * MZH_F + 4 * g, hp, lane);
       mzw_bias2<4>(net.dyn, hp, g);  // h' (un-normalised, networks.py:129-138)
+      MZH_STAMP(3);
       floatx4 hx[MZW_NT][4];
 #pragma unroll
       for (int n = 0; n < MZW_NT; ++n)
@@ -531,9 +572,11 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
         floatx4 rl[NOV][MZW_NT];
         mzw_chain<4, NOV, false>(net.rwd, hx, nullptr, nullptr, rl, lane);  // reward from h' (networks.py:132-135)
         mzw_bias2<NOV>(net.rwd, rl, g);
+        MZH_STAMP(4);
 #pragma unroll
         for (int n = 0; n < MZW_NT; ++n) rew[n] = mzw_head<NOV>(rl, n, lane);
       }
+      MZH_STAMP(5);
 #pragma unroll
       for (int n = 0; n < MZW_NT; ++n) {
         mzw_normalize(hp, n, hreg);
@@ -543,20 +586,25 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
           for (int kb = 0; kb < 4; ++kb) dst[4 * kb] = hreg[n][kb];
         }
       }
+      MZH_STAMP(6);
       {
         floatx4 pl[1][MZW_NT];
         mzw_chain<4, 1, false>(net.pol, hreg, nullptr, nullptr, pl, lane);
         mzw_bias2<1>(net.pol, pl, g);
+        MZH_STAMP(7);
 #pragma unroll
         for (int n = 0; n < MZW_NT; ++n) cpi[n] = mzw_policy(pl[0][n], lane);
       }
+      MZH_STAMP(8);
       {
         floatx4 vl[NOV][MZW_NT];
         mzw_chain<4, NOV, false>(net.val, hreg, nullptr, nullptr, vl, lane);
         mzw_bias2<NOV>(net.val, vl, g);
+        MZH_STAMP(9);
 #pragma unroll
         for (int n = 0; n < MZW_NT; ++n) val[n] = mzw_head<NOV>(vl, n, lane);
       }
+      MZH_STAMP(10);
       // the new node's 6 children (node.py:44-49): lane groups 0/1 hold pi[0..3] / pi[4..5]
       if (g < 2) {
 #pragma unroll
@@ -577,6 +625,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
       }
     }
 
+    MZH_STAMP(11);
     // ---------------- expand bookkeeping + backup (node.py:30-70): one lane per root ----------------
     if (rvalid) {
       const int enew = s + 1;
@@ -645,9 +694,14 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
       den = mmax - mmin;
       dinv = mmax > mmin ? 1.0 / (mmax - mmin) : 0.0;
     }
+    MZH_STAMP(12);
     // this simulation's tree stores (other lanes' new-block writes) before the next selection
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    if (MZW_FENCE)
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    else
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    MZH_STAMP(13);
   }
 
   // ---------------- results (mcts.py:111-126, 154-176) ----------------
@@ -739,3 +793,13 @@ hipError_t mzh_launch_wave_search(bool replay, const MzhWNet& net, const MzhSear
   if (replay) return sup33 ? launch_wave_t<true, true>(net, p, stream) : launch_wave_t<true, false>(net, p, stream);
   return sup33 ? launch_wave_t<false, true>(net, p, stream) : launch_wave_t<false, false>(net, p, stream);
 }
+
+#ifdef MZH_STAMPS
+// diagnostic build only: this translation unit's phase stamps [8 waves][MZH_NSTAMP], read and cleared
+extern "C" int mzh_diag_wave_stamps(unsigned long long* host) {
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(mzh_stamp_acc), sizeof(mzh_stamp_acc)) != hipSuccess) return -2;
+  static unsigned long long zero[8][MZH_NSTAMP] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(mzh_stamp_acc), zero, sizeof(zero)) != hipSuccess) return -2;
+  return 0;
+}
+#endif

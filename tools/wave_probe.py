@@ -1,0 +1,47 @@
+"""Phase stamps of the wave kernel (diagnostic build libmzh_diag*.so, -DMZH_STAMPS): s_memtime
+ticks per simulation for the 4 waves of workgroup 0, averaged over the S simulations."""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["MZH_LIB"] = os.environ.get("MZH_DIAG_LIB", os.path.join(ROOT, "muzero-hanoi_amd", "libmzh_diag.so"))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from muzero_hanoi_amd import _lib, engine, rng  # noqa: E402
+from muzero_hanoi_amd.networks import MuZeroNet  # noqa: E402
+
+PH = {0: "loop-top", 1: "select", 2: "gather", 3: "dyn", 4: "rwd", 5: "rwd-head", 6: "norm+store", 7: "pol",
+      8: "pol-head", 9: "val", 10: "val-head", 11: "newblock", 12: "backup", 13: "fence"}
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    S = 50
+    torch.manual_seed(0)
+    net = MuZeroNet(12, 6, 0.002, "cpu", TD_return=True)
+    eng = engine.Engine(4, S, B, 33)
+    eng.load_weights(engine.flat_weights(net.state_dict()))
+    L = _lib.lib()
+    L.mzh_diag_wave_stamps.argtypes = [ctypes.c_void_p]
+    buf = np.zeros((8, 32), np.uint64)
+    from bench import random_roots
+    obs = torch.from_numpy(random_roots(4, B, 1)).cuda()
+    noise, tie, u = (torch.from_numpy(x).cuda() for x in rng.synthetic_draws(B, deterministic=False, alpha=0.25, seed=1))
+    eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, kernel="wave")
+    torch.cuda.synchronize()
+    L.mzh_diag_wave_stamps(buf.ctypes.data)
+    eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, kernel="wave")
+    torch.cuda.synchronize()
+    L.mzh_diag_wave_stamps(buf.ctypes.data)
+    per = buf[:4, :14] / S
+    out = {f"{k}:{v}": [round(x) for x in per[:, k]] for k, v in PH.items()}
+    out["total"] = [round(x) for x in per.sum(1)]
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
