@@ -4,8 +4,9 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W             # N>1, one rank per GPU
 
-Workload: 4-disk Hanoi, 50 simulations per move, 8192 random non-goal root states per GPU
-(weak scaling: at N=8 this is the metric's 65,536-root batch), MuZeroNet(TD_return=True) with
+Workload: 4-disk Hanoi, 50 simulations per move, 65,536 random non-goal root states per GPU -- the
+metric's 65k-root batch on every GPU (weak scaling: N GPUs search N independent 65k-root batches;
+BASELINE configs[2], the same batch sharded 8 ways, is `--roots-per-gpu 8192`), MuZeroNet(TD_return=True) with
 random-init weights (torch.manual_seed(0), broadcast once), training-like search parameters
 (gamma 0.8, Dirichlet alpha 0.25 / eps 0.25, T=1, stochastic).  One step = one mzh_search launch
 over every root on the rank (root inference + 50 x {select, MFMA MLP, backup} + play policy),
@@ -42,7 +43,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--roots-per-gpu", type=int, default=8192)
+    p.add_argument("--roots-per-gpu", type=int, default=65536)
     p.add_argument("--sims", type=int, default=50)
     p.add_argument("--disks", type=int, default=4)
     p.add_argument("--seed", type=int, default=0)
@@ -169,6 +170,8 @@ def main():
     value = sims_total / dt
     flops_launch = B * (S * MLP_FLOP_PER_SIM + root_flops(N))
     achieved = flops_launch / (kern_ms * 1e-3) / 1e12
+    wave = a.kernel == "wave" or (a.kernel == "auto" and B >= 32768)  # mzh_api.hip use_wave_kernel()
+    kernel_name = "mzh_wave_kernel<false,true>" if wave else "mzh_search_kernel<32,false,true>"
     traffic = None
     if os.path.exists(a.traffic_json):
         try:
@@ -191,12 +194,12 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic: uniform random non-goal 4-disk root states, random-init MuZeroNet(TD_return=True)",
-        "config": {"workload": f"hanoi{N}_s{S}_roots{B}_per_gpu (N=8 -> {8 * B} roots = BASELINE metric batch)",
+        "config": {"workload": f"hanoi{N}_s{S}_roots{B}_per_gpu (the metric's {B}-root batch per GPU, weak scaling)",
                    "n_disks": N, "sims_per_move": S, "roots_per_gpu": B, "global_roots": world * B,
                    "parallelism": f"dp{world} (independent roots, all_gather of visits)" if world > 1 else "dp1"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": "mzh_search_kernel<32,false>", "kernel_ms": kern_ms,
+                     "kernel": kernel_name, "kernel_ms": kern_ms,
                      "flop_per_launch": flops_launch, "sel_steps_per_sim": sel_mean},
         "cpu_baseline": None,
     }

@@ -22,6 +22,7 @@ MZH_ERR_TEMPERATURE = -5
 MZH_FLAG_NP1_UCB = 1
 MZH_FLAG_KERNEL_COOP = 2  # cooperative kernel (mzh_search.hip)
 MZH_FLAG_KERNEL_WAVE = 4  # wave-independent kernel (mzh_wave.hip)
+MZH_SELFTEST_RCP = 1
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -57,6 +58,7 @@ SIGNATURES = {
     "mzh_recurrent_inference": (ctypes.c_int, [_vp, ctypes.c_int] + [_vp] * 9 + [_vp]),
     "mzh_search": (ctypes.c_int, [_vp, ctypes.POINTER(SearchArgs), _vp]),
     "mzh_search_replay": (ctypes.c_int, [_vp, ctypes.POINTER(SearchArgs), _vp]),
+    "mzh_selftest": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _vp]),
 }
 
 _lib = None

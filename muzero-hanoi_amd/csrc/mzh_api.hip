@@ -468,6 +468,13 @@ extern "C" int mzh_search(mzh_engine* eng, const mzh_search_args* args, mzh_stre
   return search_common(eng, args, stream, false);
 }
 
+extern "C" int mzh_selftest(int test, int n, int32_t* result, mzh_stream stream) {
+  if (test != MZH_SELFTEST_RCP) return fail(MZH_ERR_ARG, "selftest: unknown test %d", test);
+  if (n < 1 || n > (1 << 24) || !result) return fail(MZH_ERR_ARG, "selftest: bad n=%d / result", n);
+  hipError_t e = mzh_launch_rcp_check(n, result, (hipStream_t)stream);
+  return e == hipSuccess ? MZH_OK : hip_fail(e, "selftest launch");
+}
+
 extern "C" int mzh_search_replay(mzh_engine* eng, const mzh_search_args* args, mzh_stream stream) {
   return search_common(eng, args, stream, true);
 }

@@ -18,14 +18,28 @@
 #include "mzh_device.h"
 #include "mzh_internal.h"
 
+#ifndef MZW_PP
+#define MZW_PP 0      // 1: ping-pong schedule across the two waves of each SIMD (8-wave workgroups; measured slower: a lone wave's MFMA stream is not dense enough)
+#endif
+#ifndef MZW_PRIO
+#define MZW_PRIO 0    // ping-pong priority: 0 none, 1 static s_setprio(1) for waves 4-7, 2 M phases
+#endif
+#ifndef MZW_PPBAR
+#define MZW_PPBAR 0   // slot barrier: 0 __syncthreads (drains memory), 1 bare s_barrier
+#endif
 #ifndef MZW_WAVES
-#define MZW_WAVES 4   // waves per workgroup (independent after the start-up barrier)
+#define MZW_WAVES (MZW_PP ? 8 : 4)  // waves per workgroup
 #endif
 #ifndef MZW_STAGGER
 #define MZW_STAGGER 0  // start delay (s_sleep units of 64 cycles) of the second wave of each SIMD
 #endif
+#ifndef MZW_NT
 #define MZW_NT 2      // 16-root column tiles per wave
-#define MZW_ROOTS 32  // roots per wave
+#endif
+#define MZW_ROOTS (16 * MZW_NT)  // roots per wave
+#ifndef MZW_OCC
+#define MZW_OCC (MZW_NT == 1 ? 4 : 2)  // waves per SIMD the register budget is sized for
+#endif
 #define MZW_DC 16     // selection-path depths cached in LDS per root (deeper: HBM pathx)
 #ifndef MZW_PIN
 #define MZW_PIN 1     // pin the weight prefetch one hidden block ahead (sched_barrier)
@@ -36,6 +50,24 @@
 #define MZW_STR(x) #x
 #define MZW_XSTR(x) MZW_STR(x)
 #define MZW_UNROLL_PRAGMA _Pragma(MZW_XSTR(unroll MZW_UNROLL))
+#ifndef MZW_ONLYM
+#define MZW_ONLYM 0   // DIAGNOSTIC ONLY (wrong results): skip the tree phases, time the MLP phases alone
+#endif
+#ifndef MZW_FAKEW
+#define MZW_FAKEW 0   // DIAGNOSTIC ONLY (wrong results): every hidden block re-reads block 0's weights
+#endif
+#ifndef MZW_XLANE
+#define MZW_XLANE 1   // cross-row reductions: 1 = v_permlane16/32_swap, 0 = ds_bpermute shuffles
+#endif
+#ifndef MZW_RCP
+#define MZW_RCP 0     // 1: register reciprocal (rcp + Newton), 0: LDS table of IEEE 1/n
+#endif
+#ifndef MZW_BKPIPE
+#define MZW_BKPIPE 1  // backup: load path entry j-1 while entry j is processed
+#endif
+#ifndef MZW_SELPF
+#define MZW_SELPF 0   // selection: prefetch every child's block (towards L1) one level ahead
+#endif
 #ifndef MZW_FENCE
 #define MZW_FENCE 1   // 1: workgroup-scope fence at the end of each simulation, 0: wavefront scope
 #endif
@@ -68,7 +100,7 @@ struct MzwWave {
 };
 
 static __host__ __device__ inline size_t mzw_hdr_bytes(int S) {
-  size_t b = sizeof(float) * MZH_A * MZH_F + sizeof(double) * 2 * (size_t)(S + 3);
+  size_t b = sizeof(float) * MZH_A * MZH_F + sizeof(double) * (MZW_RCP ? 1 : 2) * (size_t)(S + 3);
   return (b + 15) & ~(size_t)15;
 }
 
@@ -78,18 +110,75 @@ __device__ __forceinline__ void mzw_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ float mzw_max4g(float v) {  // max over the 4 lane groups of a column
-  float t = __shfl_xor(v, 16);
-  v = t > v ? t : v;
-  t = __shfl_xor(v, 32);
-  return t > v ? t : v;
+// Cross-row exchange without LDS: v_permlane16_swap / v_permlane32_swap of a register with itself
+// leave {own, partner} (rows r, r^1 resp. halves h, h^1) in the two results, in the same order on
+// both lanes of a pair, so op(r[0], r[1]) is bit-identical on both (and equal to op(own, partner)
+// for the commutative max / min / add used here).
+__device__ __forceinline__ void mzw_pair16(float v, float& a, float& b) {
+  if (MZW_XLANE) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+  } else {
+    const float o = __shfl_xor(v, 16);
+    const bool lo = (threadIdx.x & 16) == 0;
+    a = lo ? v : o;
+    b = lo ? o : v;
+  }
+}
+__device__ __forceinline__ void mzw_pair32(float v, float& a, float& b) {
+  if (MZW_XLANE) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+  } else {
+    const float o = __shfl_xor(v, 32);
+    const bool lo = (threadIdx.x & 32) == 0;
+    a = lo ? v : o;
+    b = lo ? o : v;
+  }
+}
+__device__ __forceinline__ float mzw_max4g(float v) {  // max over the 4 lane groups (rows) of a column
+  float a, b;
+  mzw_pair16(v, a, b);
+  v = a > b ? a : b;
+  mzw_pair32(v, a, b);
+  return a > b ? a : b;
 }
 __device__ __forceinline__ float mzw_min4g(float v) {
-  float t = __shfl_xor(v, 16);
-  v = t < v ? t : v;
-  t = __shfl_xor(v, 32);
-  return t < v ? t : v;
+  float a, b;
+  mzw_pair16(v, a, b);
+  v = a < b ? a : b;
+  mzw_pair32(v, a, b);
+  return a < b ? a : b;
 }
+__device__ __forceinline__ float mzw_add16(float v) {  // row0 + row1 (row2 + row3)
+  float a, b;
+  mzw_pair16(v, a, b);
+  return a + b;
+}
+__device__ __forceinline__ float mzw_add32(float v) {  // rows 0-1 + rows 2-3
+  float a, b;
+  mzw_pair32(v, a, b);
+  return a + b;
+}
+
+// RN(1/n) for an integer n >= 1: v_rcp_f64 (not correctly rounded) + two Newton steps.  After the
+// first step y1 is within an ulp, so the second step's fma residual 1 - n*y1 is exact and the
+// pre-rounding error is ~e^2 < 2^-100, while 1/n is never within 2^-69 (relative) of a rounding
+// midpoint for n < 2^16: the single final rounding is RN(1/n), which the Markstein divisions need
+// (checked for every n <= 2^20 by mzh_selftest / tests/test_gpu_parity.py).  Replaces a dependent
+// LDS table lookup on the select / backup chains.
+__device__ __forceinline__ double mzw_rcp(int n, const double* inv) {
+  if (!MZW_RCP) return inv[n];
+  const double d = (double)n;
+  const double y0 = __builtin_amdgcn_rcp(d);
+  const double y1 = __builtin_fma(y0, __builtin_fma(-d, y0, 1.0), y0);
+  return __builtin_fma(y1, __builtin_fma(-d, y1, 1.0), y1);
+}
+
+__device__ const float* const kNoOhArr[4] = {nullptr, nullptr, nullptr, nullptr};
+#define kNoOh (*reinterpret_cast<const float* const(*)[MZW_NT]>(kNoOhArr))
 
 // ------------------------------------------------------------------------------------------
 // One MLP (layer1 + bias (+ one-hot column) + ReLU -> layer2, bias2 left to the caller) for the
@@ -97,8 +186,8 @@ __device__ __forceinline__ float mzw_min4g(float v) {
 // holds inputs 16kb + 4t + g, t = 0..3).  out[ot][n]: C registers of output tile ot.
 // ------------------------------------------------------------------------------------------
 template <int KB1, int NO, bool OH>
-__device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[MZW_NT][4], const float* oh0,
-                                          const float* oh1, floatx4 (&out)[NO][MZW_NT], int lane) {
+__device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[MZW_NT][4], const float* const (&oh)[MZW_NT],
+                                          floatx4 (&out)[NO][MZW_NT], int lane) {
   constexpr int FR = KB1 + NO;
   const int g = lane >> 4;
   const floatx4* S = reinterpret_cast<const floatx4*>(L.s) + lane;
@@ -107,37 +196,34 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[M
   for (int ot = 0; ot < NO; ++ot)
 #pragma unroll
     for (int n = 0; n < MZW_NT; ++n) out[ot][n] = floatx4{0.f, 0.f, 0.f, 0.f};
-  floatx4 w[FR], b, o[MZW_NT];
+  // Rolling weight buffer: slot f holds fragment f of the current hidden block and is refilled
+  // with fragment f of the next block as soon as its MFMAs are issued, so every load has the rest
+  // of this block's MFMAs (and the next block's up to f) to land.  The scheduling barriers keep
+  // the compiler from sinking the refills to their uses.
+  floatx4 w[FR];
 #pragma unroll
   for (int f = 0; f < FR; ++f) w[f] = S[f * 64];
-  b = *reinterpret_cast<const floatx4*>(B1);
-#pragma unroll
-  for (int n = 0; n < MZW_NT; ++n)
-    o[n] = OH ? *reinterpret_cast<const floatx4*>(n == 0 ? oh0 : oh1) : floatx4{0.f, 0.f, 0.f, 0.f};
   MZW_UNROLL_PRAGMA
   for (int ht = 0; ht < 16; ++ht) {
-    // next block's fragments, bias and one-hot columns: issued here and kept in flight across
-    // this block's MFMAs (the scheduling barrier stops the compiler from sinking the loads to
-    // their uses, which would expose the L2 latency once per fragment)
-    floatx4 wn[FR], bn, on[MZW_NT];
-#pragma unroll
-    for (int f = 0; f < FR; ++f) wn[f] = S[((ht + 1) * FR + f) * 64];  // block 16 is the zero pad
-    bn = *reinterpret_cast<const floatx4*>(B1 + 16 * ((ht + 1) & 15));
+    const floatx4* Sn = S + (ht + 1) * FR * 64;  // block 16 is the zero pad
+    const floatx4 b = *reinterpret_cast<const floatx4*>(B1 + 16 * ht);
+    floatx4 o[MZW_NT];
 #pragma unroll
     for (int n = 0; n < MZW_NT; ++n)
-      on[n] = OH ? *reinterpret_cast<const floatx4*>((n == 0 ? oh0 : oh1) + 16 * ((ht + 1) & 15))
-                 : floatx4{0.f, 0.f, 0.f, 0.f};
-    if (MZW_PIN) __builtin_amdgcn_sched_barrier(0);
+      o[n] = OH ? *reinterpret_cast<const floatx4*>(oh[n] + 16 * ht) : floatx4{0.f, 0.f, 0.f, 0.f};
     floatx4 acc[MZW_NT];
 #pragma unroll
     for (int n = 0; n < MZW_NT; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kb = 0; kb < KB1; ++kb)
+    for (int kb = 0; kb < KB1; ++kb) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int n = 0; n < MZW_NT; ++n)
           acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[kb][t], x[n][kb][t], acc[n], 0, 0, 0);
+      w[kb] = Sn[kb * 64];
+      if (MZW_PIN) __builtin_amdgcn_sched_barrier(0);
+    }
     floatx4 hid[MZW_NT];
 #pragma unroll
     for (int n = 0; n < MZW_NT; ++n) {
@@ -157,10 +243,8 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[M
         for (int n = 0; n < MZW_NT; ++n)
           out[ot][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[KB1 + ot][t], hid[n][t], out[ot][n], 0, 0, 0);
 #pragma unroll
-    for (int f = 0; f < FR; ++f) w[f] = wn[f];
-    b = bn;
-#pragma unroll
-    for (int n = 0; n < MZW_NT; ++n) o[n] = on[n];
+    for (int ot = 0; ot < NO; ++ot) w[KB1 + ot] = Sn[(KB1 + ot) * 64];
+    if (MZW_PIN) __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -237,8 +321,8 @@ __device__ __forceinline__ float mzw_head(const floatx4 (&l)[NO][MZW_NT], int n,
   s1 = s1 + e[5];
   s1 = s1 + e[7];
   float t = s0 + s1;
-  t = t + __shfl_xor(t, 16);
-  t = t + __shfl_xor(t, 32);
+  t = mzw_add16(t);  // (s0+s1)+(s2+s3) | (s4+s5)+(s6+s7)
+  t = mzw_add32(t);
   const float y = 1.0f / t;
   bool slow = false;
   float pk[9];
@@ -261,8 +345,8 @@ __device__ __forceinline__ float mzw_head(const floatx4 (&l)[NO][MZW_NT], int n,
   x1 = x1 + pr[5];
   x1 = x1 + pr[7];
   float xs = x0 + x1;
-  xs = xs + __shfl_xor(xs, 16);
-  xs = xs + __shfl_xor(xs, 32);
+  xs = mzw_add16(xs);
+  xs = mzw_add32(xs);
   return mzh_signed_parabolic(xs);
   }
 }
@@ -285,7 +369,7 @@ __device__ __forceinline__ floatx4 mzw_policy(const floatx4 l, int lane) {
   const float e0 = ok01 ? mzh_expf(l[0] - m) : 0.0f, e1 = ok01 ? mzh_expf(l[1] - m) : 0.0f;
   const float e2 = ok23 ? mzh_expf(l[2] - m) : 0.0f, e3 = ok23 ? mzh_expf(l[3] - m) : 0.0f;
   float t = (e0 + e1) + (e2 + e3);
-  t = t + __shfl_xor(t, 16);  // group 0: ((s0+s1)+(s2+s3)) + ((s4+s5)+(0+0))
+  t = mzw_add16(t);  // group 0: ((s0+s1)+(s2+s3)) + ((s4+s5)+(0+0))
   const float y = 1.0f / t;
   bool slow = false;
   floatx4 p;
@@ -313,10 +397,10 @@ __device__ __forceinline__ float mzw_ucb(int Nc, double Wc, float Rc, double P64
                                          const double* inv) {
   float q32 = 0.0f;
   if (Nc > 0) {
-    const double v = (double)Rc + disc * mzw_div(Wc, (double)Nc, inv[Nc]);
+    const double v = (double)Rc + disc * mzw_div(Wc, (double)Nc, mzw_rcp(Nc, inv));
     q32 = (float)(has ? mzw_div(v - mn, den, dinv) : v);
   }
-  const double w = mzw_div(tnp, (double)(Nc + 1), inv[Nc + 1]);
+  const double w = mzw_div(tnp, (double)(Nc + 1), mzw_rcp(Nc + 1, inv));
   const float u32 = p64_semantics ? (float)(P64 * w) : (float)P64 * (float)w;
   return q32 + u32;
 }
@@ -337,22 +421,23 @@ __device__ __forceinline__ int mzw_pick(const float (&u)[6], int tie, int& first
 }
 
 template <bool REPLAY, bool SUP33>
-__global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel(MzhWNet net, MzhSearchParams p) {
+__global__ __launch_bounds__(MZW_WAVES * 64, 4 * MZW_OCC / MZW_WAVES) void mzh_wave_kernel(MzhWNet net, MzhSearchParams p) {
   constexpr int NOV = SUP33 ? 3 : 1;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   const int S = p.S;
   float* ohl = reinterpret_cast<float*>(smem_raw);
   double* table = reinterpret_cast<double*>(smem_raw + sizeof(float) * MZH_A * MZH_F);
-  double* inv = table + (S + 3);
   MzwWave* wsa = reinterpret_cast<MzwWave*>(smem_raw + mzw_hdr_bytes(S));
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (scalar branches, s_setprio)
   const int g = lane >> 4, col = lane & 15;
 
   if (!REPLAY)
     for (int i = tid; i < MZH_A * MZH_F; i += MZW_WAVES * 64) ohl[i] = net.oh[i];
+  double* inv = MZW_RCP ? nullptr : table + (S + 3);
   for (int i = tid; i < S + 3; i += MZW_WAVES * 64) {
     table[i] = i < S + 2 ? p.table[i] : 0.0;
-    inv[i] = 1.0 / (double)i;  // IEEE division: correctly rounded
+    if (!MZW_RCP) inv[i] = 1.0 / (double)i;
   }
   __syncthreads();  // the only barrier: from here on every wave runs independently
   if (MZW_STAGGER > 0 && wave >= 4) {
@@ -361,7 +446,8 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
     for (int i = 0; i < MZW_STAGGER / 127; ++i) __builtin_amdgcn_s_sleep(127);
   }
   const int wr0 = (blockIdx.x * MZW_WAVES + wave) * MZW_ROOTS;
-  if (wr0 >= p.B) return;
+  const bool wactive = wr0 < p.B;  // wave-uniform
+  if (!MZW_PP && !wactive) return;  // (ping-pong: idle waves still meet every slot barrier)
   MzwWave& ws = wsa[wave];
   const double disc = p.discount;
   const bool noised = p.noise != nullptr;
@@ -391,15 +477,11 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
     cvalid[n] = croot[n] < p.B;
   }
 
-  floatx4 hreg[MZW_NT][4];  // normalised latent of the newest expanded node (B-operand order)
-#pragma unroll
-  for (int n = 0; n < MZW_NT; ++n)
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) hreg[n][kb] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   // ---------------- root: initial_inference (mcts.py:49-50) + root.expand (mcts.py:57-69) ----------------
   floatx4 rpi[MZW_NT];
-  if (!REPLAY) {
+  if (!REPLAY && wactive) {
+    floatx4 hreg[MZW_NT][4];  // the root's normalised latent (B-operand order)
     floatx4 x[MZW_NT][4];
 #pragma unroll
     for (int n = 0; n < MZW_NT; ++n)
@@ -412,10 +494,10 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
         }
     floatx4 hp[4][MZW_NT];
     switch (net.rep.kb1) {
-      case 1: mzw_chain<1, 4, false>(net.rep, x, nullptr, nullptr, hp, lane); break;
-      case 2: mzw_chain<2, 4, false>(net.rep, x, nullptr, nullptr, hp, lane); break;
-      case 3: mzw_chain<3, 4, false>(net.rep, x, nullptr, nullptr, hp, lane); break;
-      default: mzw_chain<4, 4, false>(net.rep, x, nullptr, nullptr, hp, lane); break;
+      case 1: mzw_chain<1, 4, false>(net.rep, x, kNoOh, hp, lane); break;
+      case 2: mzw_chain<2, 4, false>(net.rep, x, kNoOh, hp, lane); break;
+      case 3: mzw_chain<3, 4, false>(net.rep, x, kNoOh, hp, lane); break;
+      default: mzw_chain<4, 4, false>(net.rep, x, kNoOh, hp, lane); break;
     }
     mzw_bias2<4>(net.rep, hp, g);
 #pragma unroll
@@ -428,10 +510,10 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
       }
     }
     floatx4 pl[1][MZW_NT];
-    mzw_chain<4, 1, false>(net.pol, hreg, nullptr, nullptr, pl, lane);
+    mzw_chain<4, 1, false>(net.pol, hreg, kNoOh, pl, lane);
     mzw_bias2<1>(net.pol, pl, g);
     floatx4 vl[NOV][MZW_NT];
-    mzw_chain<4, NOV, false>(net.val, hreg, nullptr, nullptr, vl, lane);  // root value: computed, unused (mcts.py:50)
+    mzw_chain<4, NOV, false>(net.val, hreg, kNoOh, vl, lane);  // root value: computed, unused (mcts.py:50)
     (void)vl;
 #pragma unroll
     for (int n = 0; n < MZW_NT; ++n) rpi[n] = mzw_policy(pl[0][n], lane);
@@ -465,9 +547,21 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
   }
   mzw_wave_sync();
 
-  MZH_STAMP_DECL
-  for (int s = 0; s < S; ++s) {
-    MZH_STAMP(0);
+  // ---- per-simulation phases (shared by both schedules below) ----
+  int en[MZW_NT], an[MZW_NT];    // the leaf's parent (expanded index) and move, per column tile
+  // heads: evaluated inside the M phase right after their chain (only scalars stay live), or, in
+  // the ping-pong schedule, deferred to the T phase with the logits carried across
+  constexpr bool HEADS_IN_M = !MZW_PP;
+  floatx4 rl[NOV][MZW_NT], pl[1][MZW_NT], vl[NOV][MZW_NT];  // reward / policy / value logits
+  float val[MZW_NT], rew[MZW_NT];
+  floatx4 cpi[MZW_NT];
+
+  // T-phase part 1: select one leaf per root, then gather its parent latent
+  auto phase_select = [&](int s) {
+    if (MZW_ONLYM) {  // DIAGNOSTIC ONLY: no tree work (the MLP always expands the root's first child)
+      for (int n = 0; n < MZW_NT; ++n) en[n] = an[n] = 0;
+      return;
+    }
     // ---------------- select (mcts.py:75-86; node.py:72-123): one lane per root ----------------
     if (rvalid) {
       const bool has = mmax > mmin;
@@ -484,6 +578,15 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
       ws.pcR[0][rho] = ws.rR[pick][rho];
       ws.pcN[0][rho] = Np;
       int e = 0, d = 1;
+      int pf[6];
+      if (MZW_SELPF) {
+        // the next level's block is one of the root children's: bring all of them towards L1 now
+#pragma unroll
+        for (int c = 0; c < MZH_A; ++c) {
+          const int xc = ws.rX[c][rho];
+          pf[c] = *reinterpret_cast<const int*>(tb + (xc >= 0 ? xc : 0));
+        }
+      }
       while (X >= 0 && d <= S) {  // depth <= s + 1 always; the bound only guards against a corrupt tree
         e = X;
         const int4* bp = reinterpret_cast<const int4*>(tb + e);
@@ -495,6 +598,17 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
           dw[4 * k + 1] = q.y;
           dw[4 * k + 2] = q.z;
           dw[4 * k + 3] = q.w;
+        }
+        if (MZW_SELPF) {
+          // retire the previous prefetches (older than this block's loads: no extra wait), then
+          // prefetch this node's children while its UCBs are computed
+#pragma unroll
+          for (int c = 0; c < MZH_A; ++c) asm volatile("" ::"v"(pf[c]));
+#pragma unroll
+          for (int c = 0; c < MZH_A; ++c) {
+            const int xc = dw[c] >> 16;
+            pf[c] = *reinterpret_cast<const int*>(tb + (xc >= 0 ? xc : e));
+          }
         }
         double Wc[6];
         float Rc[6];
@@ -529,82 +643,85 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
         }
         ++d;
       }
+      if (MZW_SELPF) {
+#pragma unroll
+        for (int c = 0; c < MZH_A; ++c) asm volatile("" ::"v"(pf[c]));
+      }
       depth = d;
       leafE = e;
       leafA = pick;
       steps += d;
     }
-    MZH_STAMP(1);
-
-    // ---------------- expand via the network (mcts.py:88-106) ----------------
-    float val[MZW_NT], rew[MZW_NT];
-    floatx4 cpi[MZW_NT];
     if (!REPLAY) {
-      int en[MZW_NT], an[MZW_NT];
 #pragma unroll
       for (int n = 0; n < MZW_NT; ++n) {
         en[n] = __shfl(leafE, 16 * n + col);
         an[n] = __shfl(leafA, 16 * n + col);
       }
-      // parent latent (mcts.py:89-92): the node expanded by the previous simulation is in hreg
-      floatx4 x[MZW_NT][4];
+    }
+  };
+
+  // M phase: recurrent_inference's four MLPs (networks.py:96-150) as MFMA chains; the heads wait
+  // for the T phase so this phase is matrix work only
+  auto phase_mlp = [&](int s) {
+    if (REPLAY) return;
+    // the leaf's parent latent (mcts.py:89-92), stored by an earlier M phase (or the root inference)
+    floatx4 x[MZW_NT][4];
 #pragma unroll
-      for (int n = 0; n < MZW_NT; ++n) {
+    for (int n = 0; n < MZW_NT; ++n) {
+      const floatx4* src = reinterpret_cast<const floatx4*>(p.htree + ((size_t)(cvalid[n] ? croot[n] : 0) * E + en[n]) * MZH_H) + g;
 #pragma unroll
-        for (int kb = 0; kb < 4; ++kb) x[n][kb] = hreg[n][kb];
-        if (cvalid[n] && en[n] != s) {
-          const floatx4* src = reinterpret_cast<const floatx4*>(p.htree + ((size_t)croot[n] * E + en[n]) * MZH_H) + g;
+      for (int kb = 0; kb < 4; ++kb) x[n][kb] = src[4 * kb];
+    }
+    floatx4 hreg[MZW_NT][4];  // the new node's normalised latent
+    floatx4 hp[4][MZW_NT];
+    const float* ohp[MZW_NT];
 #pragma unroll
-          for (int kb = 0; kb < 4; ++kb) x[n][kb] = src[4 * kb];
+    for (int n = 0; n < MZW_NT; ++n) ohp[n] = ohl + an[n] * MZH_F + 4 * g;
+    mzw_chain<4, 4, true>(net.dyn, x, ohp, hp, lane);
+    mzw_bias2<4>(net.dyn, hp, g);  // h' (un-normalised, networks.py:129-138)
+    floatx4 hx[MZW_NT][4];
+#pragma unroll
+    for (int n = 0; n < MZW_NT; ++n)
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) hx[n][kb] = hp[kb][n];
+    mzw_chain<4, NOV, false>(net.rwd, hx, kNoOh, rl, lane);  // reward from h' (networks.py:132-135)
+    mzw_bias2<NOV>(net.rwd, rl, g);
+    if (HEADS_IN_M)
+#pragma unroll
+      for (int n = 0; n < MZW_NT; ++n) rew[n] = mzw_head<NOV>(rl, n, lane);
+#pragma unroll
+    for (int n = 0; n < MZW_NT; ++n) {
+      mzw_normalize(hp, n, hreg);
+      if (cvalid[n]) {
+        floatx4* dst = reinterpret_cast<floatx4*>(p.htree + ((size_t)croot[n] * E + s + 1) * MZH_H) + g;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) dst[4 * kb] = hreg[n][kb];
+      }
+    }
+    mzw_chain<4, 1, false>(net.pol, hreg, kNoOh, pl, lane);
+    mzw_bias2<1>(net.pol, pl, g);
+    if (HEADS_IN_M)
+#pragma unroll
+      for (int n = 0; n < MZW_NT; ++n) cpi[n] = mzw_policy(pl[0][n], lane);
+    mzw_chain<4, NOV, false>(net.val, hreg, kNoOh, vl, lane);
+    mzw_bias2<NOV>(net.val, vl, g);
+    if (HEADS_IN_M)
+#pragma unroll
+      for (int n = 0; n < MZW_NT; ++n) val[n] = mzw_head<NOV>(vl, n, lane);
+  };
+
+  // T-phase part 0: heads of simulation s, the new node's block, backup (node.py:30-70)
+  auto phase_head = [&](int s) {
+    if (MZW_ONLYM) return;  // DIAGNOSTIC ONLY
+    if (!REPLAY) {
+      if (!HEADS_IN_M)
+#pragma unroll
+        for (int n = 0; n < MZW_NT; ++n) {
+          rew[n] = mzw_head<NOV>(rl, n, lane);
+          cpi[n] = mzw_policy(pl[0][n], lane);
+          val[n] = mzw_head<NOV>(vl, n, lane);
         }
-      }
-      MZH_STAMP(2);
-      floatx4 hp[4][MZW_NT];
-      mzw_chain<4, 4, true>(net.dyn, x, ohl + an[0] * MZH_F + 4 * g, ohl + an[1] * MZH_F + 4 * g, hp, lane);
-      mzw_bias2<4>(net.dyn, hp, g);  // h' (un-normalised, networks.py:129-138)
-      MZH_STAMP(3);
-      floatx4 hx[MZW_NT][4];
-#pragma unroll
-      for (int n = 0; n < MZW_NT; ++n)
-#pragma unroll
-        for (int kb = 0; kb < 4; ++kb) hx[n][kb] = hp[kb][n];
-      {
-        floatx4 rl[NOV][MZW_NT];
-        mzw_chain<4, NOV, false>(net.rwd, hx, nullptr, nullptr, rl, lane);  // reward from h' (networks.py:132-135)
-        mzw_bias2<NOV>(net.rwd, rl, g);
-        MZH_STAMP(4);
-#pragma unroll
-        for (int n = 0; n < MZW_NT; ++n) rew[n] = mzw_head<NOV>(rl, n, lane);
-      }
-      MZH_STAMP(5);
-#pragma unroll
-      for (int n = 0; n < MZW_NT; ++n) {
-        mzw_normalize(hp, n, hreg);
-        if (cvalid[n]) {
-          floatx4* dst = reinterpret_cast<floatx4*>(p.htree + ((size_t)croot[n] * E + s + 1) * MZH_H) + g;
-#pragma unroll
-          for (int kb = 0; kb < 4; ++kb) dst[4 * kb] = hreg[n][kb];
-        }
-      }
-      MZH_STAMP(6);
-      {
-        floatx4 pl[1][MZW_NT];
-        mzw_chain<4, 1, false>(net.pol, hreg, nullptr, nullptr, pl, lane);
-        mzw_bias2<1>(net.pol, pl, g);
-        MZH_STAMP(7);
-#pragma unroll
-        for (int n = 0; n < MZW_NT; ++n) cpi[n] = mzw_policy(pl[0][n], lane);
-      }
-      MZH_STAMP(8);
-      {
-        floatx4 vl[NOV][MZW_NT];
-        mzw_chain<4, NOV, false>(net.val, hreg, nullptr, nullptr, vl, lane);
-        mzw_bias2<NOV>(net.val, vl, g);
-        MZH_STAMP(9);
-#pragma unroll
-        for (int n = 0; n < MZW_NT; ++n) val[n] = mzw_head<NOV>(vl, n, lane);
-      }
-      MZH_STAMP(10);
       // the new node's 6 children (node.py:44-49): lane groups 0/1 hold pi[0..3] / pi[4..5]
       if (g < 2) {
 #pragma unroll
@@ -624,8 +741,6 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
         }
       }
     }
-
-    MZH_STAMP(11);
     // ---------------- expand bookkeeping + backup (node.py:30-70): one lane per root ----------------
     if (rvalid) {
       const int enew = s + 1;
@@ -642,8 +757,15 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
           nb->W[c] = 0.0;
         }
       } else {
-        vv = lane < 16 ? val[0] : val[1];  // lane rho < 16: tile 0 column rho; 16..31: tile 1
-        rr = lane < 16 ? rew[0] : rew[1];
+        // root lane rho is column rho & 15 of tile rho >> 4 (every row of a column holds its scalars)
+        vv = val[0];
+        rr = rew[0];
+#pragma unroll
+        for (int n = 1; n < MZW_NT; ++n)
+          if ((lane >> 4) == n) {
+            vv = val[n];
+            rr = rew[n];
+          }
       }
       if (leafE == 0) {
         ws.rX[leafA][rho] = enew;
@@ -654,21 +776,34 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
       }
       double v = (double)vv;
       double lmax = -__builtin_inf(), lmin = __builtin_inf();
-      for (int j = depth - 1; j >= 0; --j) {
-        const int slot = j < MZW_DC ? (int)ws.path[j][rho] : (int)p.pathx[(size_t)rroot * E + j];
-        const int e = slot >> 3, a = slot & 7;
-        double Wj;
-        float Rj;
-        int Nj;
+      // path entry j: slot (parent expanded index * 8 + child) and the child's statistics at
+      // selection time; entry j - 1 is loaded while entry j is processed
+      auto load_entry = [&](int j, int& slot, double& W, float& R, int& N) {
         if (j < MZW_DC) {
-          Wj = ws.pcW[j][rho];
-          Rj = ws.pcR[j][rho];
-          Nj = ws.pcN[j][rho];
+          slot = ws.path[j][rho];
+          W = ws.pcW[j][rho];
+          R = ws.pcR[j][rho];
+          N = ws.pcN[j][rho];
         } else {
-          Wj = tb[e].W[a];
-          Rj = tb[e].R[a];
-          Nj = tb[e].nx[a].N;
+          slot = p.pathx[(size_t)rroot * E + j];
+          const int e = slot >> 3, a = slot & 7;
+          W = tb[e].W[a];
+          R = tb[e].R[a];
+          N = tb[e].nx[a].N;
         }
+      };
+      int slot;
+      double Wj;
+      float Rj;
+      int Nj;
+      if (MZW_BKPIPE) load_entry(depth - 1, slot, Wj, Rj, Nj);
+      for (int j = depth - 1; j >= 0; --j) {
+        int slot_n = 0, Nj_n = 0;
+        double Wj_n = 0.0;
+        float Rj_n = 0.0f;
+        if (MZW_BKPIPE && j > 0) load_entry(j - 1, slot_n, Wj_n, Rj_n, Nj_n);
+        if (!MZW_BKPIPE) load_entry(j, slot, Wj, Rj, Nj);
+        const int e = slot >> 3, a = slot & 7;
         const double rw = (j == depth - 1) ? (double)rr : (double)Rj;
         const double Wn = Wj + v;
         const int Nn = Nj + 1;
@@ -679,14 +814,18 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
           tb[e].W[a] = Wn;
           tb[e].nx[a].N = (uint16_t)Nn;
         }
-        const double q = rw + disc * mzw_div(Wn, (double)Nn, inv[Nn]);
+        const double q = rw + disc * mzw_div(Wn, (double)Nn, mzw_rcp(Nn, inv));
         lmax = q > lmax ? q : lmax;
         lmin = q < lmin ? q : lmin;
         v = rw + disc * v;
+        slot = slot_n;
+        Wj = Wj_n;
+        Rj = Rj_n;
+        Nj = Nj_n;
       }
       rootW = rootW + v;
       rootN = rootN + 1;
-      const double q = 0.0 + disc * mzw_div(rootW, (double)rootN, inv[rootN]);  // root rwd = 0.0
+      const double q = 0.0 + disc * mzw_div(rootW, (double)rootN, mzw_rcp(rootN, inv));  // root rwd = 0.0
       lmax = q > lmax ? q : lmax;
       lmin = q < lmin ? q : lmin;
       mmax = lmax > mmax ? lmax : mmax;
@@ -694,14 +833,55 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
       den = mmax - mmin;
       dinv = mmax > mmin ? 1.0 / (mmax - mmin) : 0.0;
     }
-    MZH_STAMP(12);
-    // this simulation's tree stores (other lanes' new-block writes) before the next selection
-    if (MZW_FENCE)
+  };
+
+  MZH_STAMP_DECL
+  if (!MZW_PP) {
+    for (int s = 0; s < S; ++s) {
+      MZH_STAMP(4);
+      phase_select(s);
+      MZH_STAMP(0);
+      phase_mlp(s);
+      MZH_STAMP(1);
+      phase_head(s);
+      MZH_STAMP(2);
+      // this simulation's tree stores (other lanes' new-block writes) before the next selection
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-    else
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    MZH_STAMP(13);
+      __builtin_amdgcn_wave_barrier();
+    }
+  } else {
+    // Ping-pong: waves w and w + 4 share a SIMD.  The second half runs one slot behind the first,
+    // so in every slot one wave of each SIMD is in an M phase (matrix pipe) while its partner is
+    // in a T phase (heads, backup, selection: latency-bound L2 / LDS / fp64 work).  A wave's
+    // sequence is T0 = select(0), M0, T1 = head(0) + select(1), M1, ..., M(S-1), TS = head(S-1).
+    const int lag = wave >= MZW_WAVES / 2 ? 1 : 0;
+    if (MZW_PRIO == 1 && lag) __builtin_amdgcn_s_setprio(1);  // the younger half (guide: static priority)
+    for (int k = 0; k < 2 * S + 2; ++k) {
+      const int kk = k - lag;
+      if (wactive && kk >= 0 && kk <= 2 * S) {
+        if ((kk & 1) == 0) {
+          const int j = kk >> 1;
+          if (j >= 1) phase_head(j - 1);
+          MZH_STAMP(2);
+          if (j < S) phase_select(j);
+          MZH_STAMP(0);
+        } else {
+          if (MZW_PRIO == 2) __builtin_amdgcn_s_setprio(1);  // matrix phase wins VALU arbitration
+          phase_mlp(kk >> 1);
+          if (MZW_PRIO == 2) __builtin_amdgcn_s_setprio(0);
+          MZH_STAMP(1);
+        }
+      }
+      // slot boundary; the same wave's stores are ordered for the next phase either way
+      if (MZW_PPBAR) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      } else {
+        __syncthreads();
+      }
+      MZH_STAMP(3);
+    }
   }
 
   // ---------------- results (mcts.py:111-126, 154-176) ----------------
@@ -772,6 +952,16 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
     }
     if (p.action) p.action[root] = act;
   }
+}
+
+// mzh_selftest(MZH_SELFTEST_RCP): mzw_rcp(n) == IEEE 1.0 / n for every n in [1, nmax]
+__global__ void mzw_rcp_check_kernel(int nmax, int32_t* bad) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (n <= nmax && mzw_rcp(n, nullptr) != 1.0 / (double)n) atomicAdd(bad, 1);
+}
+hipError_t mzh_launch_rcp_check(int nmax, int32_t* bad, hipStream_t stream) {
+  hipLaunchKernelGGL(mzw_rcp_check_kernel, dim3((nmax + 255) / 256), dim3(256), 0, stream, nmax, bad);
+  return hipGetLastError();
 }
 
 size_t mzh_wave_smem_bytes(int S) { return mzw_hdr_bytes(S) + sizeof(MzwWave) * MZW_WAVES; }

@@ -35,6 +35,7 @@ def main():
     p.add_argument("--roots", type=int, default=8192)
     p.add_argument("--sims", type=int, default=50)
     p.add_argument("--disks", type=int, default=4)
+    p.add_argument("--kernel", default=None)
     a = p.parse_args()
     from bench import random_roots
     from muzero_hanoi_amd import engine, rng
@@ -50,7 +51,7 @@ def main():
     noise, tie, u = (torch.from_numpy(x).to(dev) for x in rng.synthetic_draws(B, deterministic=False, alpha=0.25, seed=1))
     out = eng.alloc_search_outputs(B, S)
     res = {}
-    res["full_ms"] = timeit(lambda: eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, out=out))
+    res["full_ms"] = timeit(lambda: eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, out=out, kernel=a.kernel))
     # replay inputs shaped like real network outputs
     g = np.random.default_rng(0)
     pi = g.dirichlet(np.ones(6), size=(B, S)).astype(np.float32)
@@ -58,7 +59,7 @@ def main():
               pi=torch.from_numpy(pi).to(dev),
               reward=torch.from_numpy(g.normal(0, 0.05, (B, S)).astype(np.float32)).to(dev),
               value=torch.from_numpy(g.normal(0, 1, (B, S)).astype(np.float32)).to(dev))
-    res["tree_ms"] = timeit(lambda: eng.search(S, replay=rp, tie_idx=tie, noise=noise, action_u=u, out=out))
+    res["tree_ms"] = timeit(lambda: eng.search(S, replay=rp, tie_idx=tie, noise=noise, action_u=u, out=out, kernel=a.kernel))
     h = torch.rand((B, 64), device=dev)
     act = torch.randint(0, 6, (B,), dtype=torch.int32, device=dev)
     res["mlp_rec_one_ms"] = timeit(lambda: eng.recurrent_inference(h, act))

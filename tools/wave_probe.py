@@ -14,8 +14,7 @@ import torch  # noqa: E402
 from muzero_hanoi_amd import _lib, engine, rng  # noqa: E402
 from muzero_hanoi_amd.networks import MuZeroNet  # noqa: E402
 
-PH = {0: "loop-top", 1: "select", 2: "gather", 3: "dyn", 4: "rwd", 5: "rwd-head", 6: "norm+store", 7: "pol",
-      8: "pol-head", 9: "val", 10: "val-head", 11: "newblock", 12: "backup", 13: "fence"}
+PH = {0: "select", 1: "mlp", 2: "head+backup", 3: "barrier", 4: "loop-top"}
 
 
 def main():
@@ -37,7 +36,7 @@ def main():
     eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, kernel="wave")
     torch.cuda.synchronize()
     L.mzh_diag_wave_stamps(buf.ctypes.data)
-    per = buf[:4, :14] / S
+    per = buf[:8, :5] / S  # 8 waves (ping-pong workgroup); the 4-wave build leaves rows 4-7 zero
     out = {f"{k}:{v}": [round(x) for x in per[:, k]] for k, v in PH.items()}
     out["total"] = [round(x) for x in per.sum(1)]
     print(json.dumps(out))
