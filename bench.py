@@ -194,7 +194,8 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic: uniform random non-goal 4-disk root states, random-init MuZeroNet(TD_return=True)",
-        "config": {"workload": f"hanoi{N}_s{S}_roots{B}_per_gpu (the metric's {B}-root batch per GPU, weak scaling)",
+        "config": {"workload": f"hanoi{N}_s{S}_roots{B}_per_gpu" + (" (the metric's 65k-root batch on every GPU, weak scaling)"
+                                                                   if B == 65536 else " (weak scaling)"),
                    "n_disks": N, "sims_per_move": S, "roots_per_gpu": B, "global_roots": world * B,
                    "parallelism": f"dp{world} (independent roots, all_gather of visits)" if world > 1 else "dp1"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -7,6 +7,7 @@ import os
 import sys
 
 ROOT = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+KERNEL = sys.argv[2] if len(sys.argv) > 2 else "mzh_wave_kernel"  # substring of the dominant kernel
 
 
 def newest(pattern):
@@ -18,7 +19,7 @@ out = {}
 ks = newest("prof_trace/*/*_kernel_stats.csv")
 if ks:
     for r in csv.DictReader(open(ks)):
-        if "search_kernel" in r["Name"]:
+        if KERNEL in r["Name"]:
             out["kernel"] = r["Name"]
             out["calls"] = int(r["Calls"])
             out["avg_ns"] = float(r["AverageNs"])
@@ -28,10 +29,13 @@ for p in ("hit", "fetch", "write", "sq"):
         continue
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
-        if "search_kernel" in r["Kernel_Name"]:
-            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    for k, v in agg.items():
-        out[k] = sum(v) / len(v)
+        if KERNEL in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append((r["Dispatch_Id"], float(r["Counter_Value"])))
+    for k, v in agg.items():  # sum over the per-XCD / per-SE rows of one dispatch, mean over dispatches
+        per = collections.defaultdict(float)
+        for d, x in v:
+            per[d] += x
+        out[k] = sum(per.values()) / len(per)
 if "TCC_HIT_sum" in out:
     out["l2_hit_rate"] = out["TCC_HIT_sum"] / (out["TCC_HIT_sum"] + out["TCC_MISS_sum"])
 if "FETCH_SIZE" in out:
