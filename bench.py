@@ -171,7 +171,8 @@ def main():
     flops_launch = B * (S * MLP_FLOP_PER_SIM + root_flops(N))
     achieved = flops_launch / (kern_ms * 1e-3) / 1e12
     wave = a.kernel == "wave" or (a.kernel == "auto" and B >= 32768)  # mzh_api.hip use_wave_kernel()
-    kernel_name = "mzh_wave_kernel<false,true>" if wave else "mzh_search_kernel<32,false,true>"
+    coop_rows = 32 if B >= 8192 else 16  # mzh_api.hip pick_rows()
+    kernel_name = "mzh_wave_kernel<false,true>" if wave else f"mzh_search_kernel<{coop_rows},false,*>"
     traffic = None
     if os.path.exists(a.traffic_json):
         try:

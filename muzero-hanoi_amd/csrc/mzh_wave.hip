@@ -169,13 +169,14 @@ __device__ __forceinline__ float mzw_add32(float v) {  // rows 0-1 + rows 2-3
 // midpoint for n < 2^16: the single final rounding is RN(1/n), which the Markstein divisions need
 // (checked for every n <= 2^20 by mzh_selftest / tests/test_gpu_parity.py).  Replaces a dependent
 // LDS table lookup on the select / backup chains.
-__device__ __forceinline__ double mzw_rcp(int n, const double* inv) {
-  if (!MZW_RCP) return inv[n];
+__device__ __forceinline__ double mzw_rcp_reg(int n) {
   const double d = (double)n;
   const double y0 = __builtin_amdgcn_rcp(d);
   const double y1 = __builtin_fma(y0, __builtin_fma(-d, y0, 1.0), y0);
   return __builtin_fma(y1, __builtin_fma(-d, y1, 1.0), y1);
 }
+// the search kernel's RN(1/n): LDS table of IEEE 1/n (default) or the register form above
+__device__ __forceinline__ double mzw_rcp(int n, const double* inv) { return MZW_RCP ? mzw_rcp_reg(n) : inv[n]; }
 
 __device__ const float* const kNoOhArr[4] = {nullptr, nullptr, nullptr, nullptr};
 #define kNoOh (*reinterpret_cast<const float* const(*)[MZW_NT]>(kNoOhArr))
@@ -957,7 +958,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 4 * MZW_OCC / MZW_WAVES) void mzh_w
 // mzh_selftest(MZH_SELFTEST_RCP): mzw_rcp(n) == IEEE 1.0 / n for every n in [1, nmax]
 __global__ void mzw_rcp_check_kernel(int nmax, int32_t* bad) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x + 1;
-  if (n <= nmax && mzw_rcp(n, nullptr) != 1.0 / (double)n) atomicAdd(bad, 1);
+  if (n <= nmax && mzw_rcp_reg(n) != 1.0 / (double)n) atomicAdd(bad, 1);
 }
 hipError_t mzh_launch_rcp_check(int nmax, int32_t* bad, hipStream_t stream) {
   hipLaunchKernelGGL(mzw_rcp_check_kernel, dim3((nmax + 255) / 256), dim3(256), 0, stream, nmax, bad);
