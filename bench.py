@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-gather", action="store_true")
     p.add_argument("--kernel", choices=["auto", "coop", "wave"], default="auto")
+    p.add_argument("--dist-backend", default="nccl",
+                   help="nccl (= RCCL, one rank per GPU); gloo lets ranks share a GPU to rehearse the N>1 path")
     p.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
@@ -97,13 +99,20 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world and world > 1:
         raise SystemExit(f"--gpus {a.gpus} != WORLD_SIZE {world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    if a.dist_backend == "nccl" and world > 1 and local >= ndev:
+        raise SystemExit(f"LOCAL_RANK {local} but only {ndev} GPUs (RCCL needs one GPU per rank)")
+    gpu = local % ndev
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(a.dist_backend)
 
     from muzero_hanoi_amd import distributed as mdist
     from muzero_hanoi_amd import engine, rng
@@ -116,7 +125,7 @@ def main():
     flat = engine.flat_weights(net.state_dict())
     if dist is not None:
         flat = mdist.broadcast_weights(flat, dev)  # weights broadcast once (~0.5 MB)
-    eng = engine.Engine(N, S, B, 33, device=local)
+    eng = engine.Engine(N, S, B, 33, device=gpu)
     eng.load_weights(flat)
 
     # inputs for the GLOBAL batch in global root order, then this rank's contiguous shard
