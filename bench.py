@@ -48,7 +48,7 @@ def parse():
     p.add_argument("--disks", type=int, default=4)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-gather", action="store_true")
-    p.add_argument("--kernel", choices=["auto", "coop", "wave"], default="auto")
+    p.add_argument("--kernel", choices=["auto", "coop", "wave", "wave16"], default="auto")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, one rank per GPU); gloo lets ranks share a GPU to rehearse the N>1 path")
     p.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
@@ -179,9 +179,10 @@ def main():
     value = sims_total / dt
     flops_launch = B * (S * MLP_FLOP_PER_SIM + root_flops(N))
     achieved = flops_launch / (kern_ms * 1e-3) / 1e12
-    wave = a.kernel == "wave" or (a.kernel == "auto" and B >= 32768)  # mzh_api.hip use_wave_kernel()
-    coop_rows = 32 if B >= 8192 else 16  # mzh_api.hip pick_rows()
-    kernel_name = "mzh_wave_kernel<false,true>" if wave else f"mzh_search_kernel<{coop_rows},false,*>"
+    kern_sel = a.kernel if a.kernel != "auto" else ("wave" if B >= 24576 else "wave16" if B >= 16384 else "coop")
+    coop_rows = 32 if B >= 8192 else 16  # mzh_api.hip choose_kernel() / pick_rows()
+    kernel_name = {"wave": "mzh_wave_kernel<2,false,true>", "wave16": "mzh_wave_kernel<1,false,true>",
+                   "coop": f"mzh_search_kernel<{coop_rows},false,*>"}[kern_sel]
     traffic = None
     if os.path.exists(a.traffic_json):
         try:

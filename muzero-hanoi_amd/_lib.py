@@ -21,7 +21,8 @@ MZH_ERR_STATE = -4
 MZH_ERR_TEMPERATURE = -5
 MZH_FLAG_NP1_UCB = 1
 MZH_FLAG_KERNEL_COOP = 2  # cooperative kernel (mzh_search.hip)
-MZH_FLAG_KERNEL_WAVE = 4  # wave-independent kernel (mzh_wave.hip)
+MZH_FLAG_KERNEL_WAVE = 4  # wave-independent kernel (mzh_wave.hip), 32 roots per wave
+MZH_FLAG_KERNEL_WAVE16 = 8  # wave-independent kernel, 16 roots per wave
 MZH_SELFTEST_RCP = 1
 
 _vp = ctypes.c_void_p

@@ -404,20 +404,28 @@ extern "C" int mzh_recurrent_inference(mzh_engine* eng, int B, const float* h_in
 // ---- search ----
 static const size_t kMaxLds = 163840;
 
-// kernel choice: the wave-independent kernel (mzh_wave.hip) needs >= 2 waves of 32 roots per SIMD
-// to overlap its tree and MFMA phases; smaller batches run the cooperative kernel (mzh_search.hip)
-// whose 4 waves share one 32-root MLP tile.  MZH_FLAG_KERNEL_* (or MZH_KERNEL=coop|wave) force one.
-static const int kWaveMinRoots = 32768;
-static bool use_wave_kernel(int B, uint32_t flags) {
-  if (flags & MZH_FLAG_KERNEL_WAVE) return true;
-  if (flags & MZH_FLAG_KERNEL_COOP) return false;
+// kernel choice: the wave-independent kernel (mzh_wave.hip) with 32 roots per wave once the batch
+// gives >= 1024 waves (one per SIMD, two co-resident per SIMD at 65k roots), with 16 roots per wave
+// for mid-size batches (>= 1024 such waves), else the cooperative kernel (mzh_search.hip) whose 4
+// waves share one 32-root MLP tile.  MZH_FLAG_KERNEL_* (or MZH_KERNEL=coop|wave|wave16) force one.
+static const int kWaveMinRoots = 24576, kWave16MinRoots = 16384;  // measured crossovers
+struct KernelChoice {
+  bool wave;
+  int nt;  // wave kernel: 16-root column tiles per wave
+};
+static KernelChoice choose_kernel(int B, uint32_t flags) {
+  if (flags & MZH_FLAG_KERNEL_WAVE16) return {true, 1};
+  if (flags & MZH_FLAG_KERNEL_WAVE) return {true, 2};
+  if (flags & MZH_FLAG_KERNEL_COOP) return {false, 0};
   static const int forced = [] {
     const char* v = getenv("MZH_KERNEL");
     if (!v) return 0;
-    return strcmp(v, "wave") == 0 ? 1 : strcmp(v, "coop") == 0 ? -1 : 0;
+    return strcmp(v, "wave") == 0 ? 2 : strcmp(v, "wave16") == 0 ? 1 : strcmp(v, "coop") == 0 ? -1 : 0;
   }();
-  if (forced) return forced > 0;
-  return B >= kWaveMinRoots;
+  if (forced) return forced > 0 ? KernelChoice{true, forced} : KernelChoice{false, 0};
+  if (B >= kWaveMinRoots) return {true, 2};
+  if (B >= kWave16MinRoots) return {true, 1};
+  return {false, 0};
 }
 
 static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream stream, bool replay) {
@@ -438,10 +446,11 @@ static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream s
   }
   if (!a->deterministic && !a->action_u && a->action)
     return fail(MZH_ERR_ARG, "stochastic action selection needs action_u");
-  const bool wave = use_wave_kernel(a->B, a->flags);
+  const KernelChoice kc = choose_kernel(a->B, a->flags);
+  const bool wave = kc.wave;
   int R = pick_rows(a->B);
   if (wave) {
-    if (mzh_wave_smem_bytes(a->n_sims) > kMaxLds)
+    if (mzh_wave_smem_bytes(a->n_sims, kc.nt) > kMaxLds)
       return fail(MZH_ERR_CAPACITY, "n_sims=%d exceeds the wave kernel's LDS table budget", a->n_sims);
   } else {
     if (mzh_search_smem_bytes(R, a->n_sims) > kMaxLds) R = 16;
@@ -459,7 +468,7 @@ static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream s
   p.tree = eng->tree; p.htree = eng->htree; p.pathx = eng->pathx; p.table = eng->table;
   p.visits = a->visits; p.root_q = a->root_q; p.minmax_out = a->minmax_out; p.extra_ties = a->extra_ties;
   p.action = a->action; p.pi = a->pi; p.latent = a->latent; p.latent_len = a->latent_len; p.sel_steps = a->sel_steps;
-  hipError_t e = wave ? mzh_launch_wave_search(replay, eng->wnet, p, (hipStream_t)stream)
+  hipError_t e = wave ? mzh_launch_wave_search(kc.nt, replay, eng->wnet, p, (hipStream_t)stream)
                       : mzh_launch_search(R, replay, eng->net, p, (hipStream_t)stream);
   return e == hipSuccess ? MZH_OK : hip_fail(e, "search launch");
 }

@@ -101,9 +101,9 @@ struct MzhWNet {
   int support, in_dim;
 };
 
-size_t mzh_wave_smem_bytes(int S);
+size_t mzh_wave_smem_bytes(int S, int nt);
 hipError_t mzh_launch_rcp_check(int nmax, int32_t* bad, hipStream_t stream);
-hipError_t mzh_launch_wave_search(bool replay, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream);
+hipError_t mzh_launch_wave_search(int nt, bool replay, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream);
 size_t mzh_search_smem_bytes(int R, int S);
 hipError_t mzh_launch_search(int R, bool replay, const MzhNet& net, const MzhSearchParams& p, hipStream_t stream);
 hipError_t mzh_launch_infer(int R, bool recurrent, const MzhNet& net, const MzhInferParams& p, hipStream_t stream);

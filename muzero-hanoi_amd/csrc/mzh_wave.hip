@@ -30,16 +30,9 @@
 #ifndef MZW_WAVES
 #define MZW_WAVES (MZW_PP ? 8 : 4)  // waves per workgroup
 #endif
-#ifndef MZW_STAGGER
-#define MZW_STAGGER 0  // start delay (s_sleep units of 64 cycles) of the second wave of each SIMD
-#endif
-#ifndef MZW_NT
-#define MZW_NT 2      // 16-root column tiles per wave
-#endif
-#define MZW_ROOTS (16 * MZW_NT)  // roots per wave
-#ifndef MZW_OCC
-#define MZW_OCC (MZW_NT == 1 ? 4 : 2)  // waves per SIMD the register budget is sized for
-#endif
+// NT (template parameter): 16-root MFMA column tiles per wave -- 2 (32 roots) for large batches,
+// 1 (16 roots: half the weight reuse) so that mid-size batches still give every SIMD a wave;
+// both are built for 2 waves per SIMD (256 VGPRs)
 #define MZW_DC 16     // selection-path depths cached in LDS per root (deeper: HBM pathx)
 #ifndef MZW_PIN
 #define MZW_PIN 1     // pin the weight prefetch one hidden block ahead (sched_barrier)
@@ -52,9 +45,6 @@
 #define MZW_UNROLL_PRAGMA _Pragma(MZW_XSTR(unroll MZW_UNROLL))
 #ifndef MZW_ONLYM
 #define MZW_ONLYM 0   // DIAGNOSTIC ONLY (wrong results): skip the tree phases, time the MLP phases alone
-#endif
-#ifndef MZW_FAKEW
-#define MZW_FAKEW 0   // DIAGNOSTIC ONLY (wrong results): every hidden block re-reads block 0's weights
 #endif
 #ifndef MZW_XLANE
 #define MZW_XLANE 1   // cross-row reductions: 1 = v_permlane16/32_swap, 0 = ds_bpermute shuffles
@@ -87,16 +77,17 @@ struct __align__(128) MzwBlock {
 static_assert(sizeof(MzwBlock) == 128, "block layout");
 
 // per-wave LDS: the roots' own children (SoA, lane = root: conflict-free) and the path cache
+template <int ROOTS>
 struct MzwWave {
-  double rW[6][MZW_ROOTS];
-  double rP[6][MZW_ROOTS];  // fp64 prior (Dirichlet-mixed or the widened fp32 prior)
-  float rR[6][MZW_ROOTS];
-  int rN[6][MZW_ROOTS];
-  int rX[6][MZW_ROOTS];
-  double pcW[MZW_DC][MZW_ROOTS];  // chosen child's statistics at each depth (select snapshot)
-  float pcR[MZW_DC][MZW_ROOTS];
-  int pcN[MZW_DC][MZW_ROOTS];
-  uint16_t path[MZW_DC][MZW_ROOTS];  // slot = parent expanded index * 8 + child
+  double rW[6][ROOTS];
+  double rP[6][ROOTS];  // fp64 prior (Dirichlet-mixed or the widened fp32 prior)
+  float rR[6][ROOTS];
+  int rN[6][ROOTS];
+  int rX[6][ROOTS];
+  double pcW[MZW_DC][ROOTS];  // chosen child's statistics at each depth (select snapshot)
+  float pcR[MZW_DC][ROOTS];
+  int pcN[MZW_DC][ROOTS];
+  uint16_t path[MZW_DC][ROOTS];  // slot = parent expanded index * 8 + child
 };
 
 static __host__ __device__ inline size_t mzw_hdr_bytes(int S) {
@@ -178,17 +169,15 @@ __device__ __forceinline__ double mzw_rcp_reg(int n) {
 // the search kernel's RN(1/n): LDS table of IEEE 1/n (default) or the register form above
 __device__ __forceinline__ double mzw_rcp(int n, const double* inv) { return MZW_RCP ? mzw_rcp_reg(n) : inv[n]; }
 
-__device__ const float* const kNoOhArr[4] = {nullptr, nullptr, nullptr, nullptr};
-#define kNoOh (*reinterpret_cast<const float* const(*)[MZW_NT]>(kNoOhArr))
 
 // ------------------------------------------------------------------------------------------
 // One MLP (layer1 + bias (+ one-hot column) + ReLU -> layer2, bias2 left to the caller) for the
 // wave's 2 column tiles.  x[n][kb] = the B operand of column tile n, k-block kb (lane group g
 // holds inputs 16kb + 4t + g, t = 0..3).  out[ot][n]: C registers of output tile ot.
 // ------------------------------------------------------------------------------------------
-template <int KB1, int NO, bool OH>
-__device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[MZW_NT][4], const float* const (&oh)[MZW_NT],
-                                          floatx4 (&out)[NO][MZW_NT], int lane) {
+template <int NT, int KB1, int NO, bool OH>
+__device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[NT][4], const float* const (&oh)[NT],
+                                          floatx4 (&out)[NO][NT], int lane) {
   constexpr int FR = KB1 + NO;
   const int g = lane >> 4;
   const floatx4* S = reinterpret_cast<const floatx4*>(L.s) + lane;
@@ -196,7 +185,7 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[M
 #pragma unroll
   for (int ot = 0; ot < NO; ++ot)
 #pragma unroll
-    for (int n = 0; n < MZW_NT; ++n) out[ot][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NT; ++n) out[ot][n] = floatx4{0.f, 0.f, 0.f, 0.f};
   // Rolling weight buffer: slot f holds fragment f of the current hidden block and is refilled
   // with fragment f of the next block as soon as its MFMAs are issued, so every load has the rest
   // of this block's MFMAs (and the next block's up to f) to land.  The scheduling barriers keep
@@ -208,26 +197,26 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[M
   for (int ht = 0; ht < 16; ++ht) {
     const floatx4* Sn = S + (ht + 1) * FR * 64;  // block 16 is the zero pad
     const floatx4 b = *reinterpret_cast<const floatx4*>(B1 + 16 * ht);
-    floatx4 o[MZW_NT];
+    floatx4 o[NT];
 #pragma unroll
-    for (int n = 0; n < MZW_NT; ++n)
+    for (int n = 0; n < NT; ++n)
       o[n] = OH ? *reinterpret_cast<const floatx4*>(oh[n] + 16 * ht) : floatx4{0.f, 0.f, 0.f, 0.f};
-    floatx4 acc[MZW_NT];
+    floatx4 acc[NT];
 #pragma unroll
-    for (int n = 0; n < MZW_NT; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NT; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kb = 0; kb < KB1; ++kb) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int n = 0; n < MZW_NT; ++n)
+        for (int n = 0; n < NT; ++n)
           acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[kb][t], x[n][kb][t], acc[n], 0, 0, 0);
       w[kb] = Sn[kb * 64];
       if (MZW_PIN) __builtin_amdgcn_sched_barrier(0);
     }
-    floatx4 hid[MZW_NT];
+    floatx4 hid[NT];
 #pragma unroll
-    for (int n = 0; n < MZW_NT; ++n) {
+    for (int n = 0; n < NT; ++n) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float v = acc[n][i];
@@ -241,7 +230,7 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[M
 #pragma unroll
       for (int ot = 0; ot < NO; ++ot)
 #pragma unroll
-        for (int n = 0; n < MZW_NT; ++n)
+        for (int n = 0; n < NT; ++n)
           out[ot][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[KB1 + ot][t], hid[n][t], out[ot][n], 0, 0, 0);
 #pragma unroll
     for (int ot = 0; ot < NO; ++ot) w[KB1 + ot] = Sn[(KB1 + ot) * 64];
@@ -249,20 +238,21 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[M
   }
 }
 
-template <int NO>
-__device__ __forceinline__ void mzw_bias2(const MzhWMlp& L, floatx4 (&out)[NO][MZW_NT], int g) {
+template <int NT, int NO>
+__device__ __forceinline__ void mzw_bias2(const MzhWMlp& L, floatx4 (&out)[NO][NT], int g) {
 #pragma unroll
   for (int ot = 0; ot < NO; ++ot) {
     const floatx4 b = *reinterpret_cast<const floatx4*>(L.b2 + 16 * ot + 4 * g);
 #pragma unroll
-    for (int n = 0; n < MZW_NT; ++n)
+    for (int n = 0; n < NT; ++n)
 #pragma unroll
       for (int i = 0; i < 4; ++i) out[ot][n][i] = out[ot][n][i] + b[i];
   }
 }
 
 // normalize_h_state (networks.py:191-196) of one column: lane group g holds 16 of the 64 units
-__device__ __forceinline__ void mzw_normalize(const floatx4 (&hp)[4][MZW_NT], int n, floatx4 (&hn)[MZW_NT][4]) {
+template <int NT>
+__device__ __forceinline__ void mzw_normalize(const floatx4 (&hp)[4][NT], int n, floatx4 (&hn)[NT][4]) {
   float mn = hp[0][n][0], mx = hp[0][n][0];
 #pragma unroll
   for (int ot = 0; ot < 4; ++ot)
@@ -293,8 +283,8 @@ __device__ __forceinline__ void mzw_normalize(const floatx4 (&hp)[4][MZW_NT], in
 // Slot s = 4ot + i of lane group g holds logit k = 2g + (s & 1) + 8(s >> 1) (slot 8 only for g = 0),
 // so the lane's two sequential partials are the oracle's s_{2g}, s_{2g+1} and the cross-group
 // adds reproduce ((s0+s1)+(s2+s3))+((s4+s5)+(s6+s7)).
-template <int NO>
-__device__ __forceinline__ float mzw_head(const floatx4 (&l)[NO][MZW_NT], int n, int lane) {
+template <int NT, int NO>
+__device__ __forceinline__ float mzw_head(const floatx4 (&l)[NO][NT], int n, int lane) {
   const int g = lane >> 4;
   if constexpr (NO == 1) {
     return __shfl(l[0][n][0], lane & 15);  // support 1: the raw logit (networks.py:146-148)
@@ -421,14 +411,16 @@ __device__ __forceinline__ int mzw_pick(const float (&u)[6], int tie, int& first
   return six ? tie : first;
 }
 
-template <bool REPLAY, bool SUP33>
-__global__ __launch_bounds__(MZW_WAVES * 64, 4 * MZW_OCC / MZW_WAVES) void mzh_wave_kernel(MzhWNet net, MzhSearchParams p) {
+template <int NT, bool REPLAY, bool SUP33>
+__global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel(MzhWNet net, MzhSearchParams p) {
   constexpr int NOV = SUP33 ? 3 : 1;
+  constexpr int ROOTS = 16 * NT;  // roots per wave
+  const float* const noh[NT] = {};  // "no one-hot column" for the chains that take none
   extern __shared__ __align__(16) unsigned char smem_raw[];
   const int S = p.S;
   float* ohl = reinterpret_cast<float*>(smem_raw);
   double* table = reinterpret_cast<double*>(smem_raw + sizeof(float) * MZH_A * MZH_F);
-  MzwWave* wsa = reinterpret_cast<MzwWave*>(smem_raw + mzw_hdr_bytes(S));
+  MzwWave<ROOTS>* wsa = reinterpret_cast<MzwWave<ROOTS>*>(smem_raw + mzw_hdr_bytes(S));
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (scalar branches, s_setprio)
   const int g = lane >> 4, col = lane & 15;
@@ -441,15 +433,10 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 4 * MZW_OCC / MZW_WAVES) void mzh_w
     if (!MZW_RCP) inv[i] = 1.0 / (double)i;
   }
   __syncthreads();  // the only barrier: from here on every wave runs independently
-  if (MZW_STAGGER > 0 && wave >= 4) {
-    // waves w and w + 4 share a SIMD: start the second one about a tree phase later so the two
-    // alternate between MFMA and tree work instead of running their phases in lockstep
-    for (int i = 0; i < MZW_STAGGER / 127; ++i) __builtin_amdgcn_s_sleep(127);
-  }
-  const int wr0 = (blockIdx.x * MZW_WAVES + wave) * MZW_ROOTS;
+  const int wr0 = (blockIdx.x * MZW_WAVES + wave) * ROOTS;
   const bool wactive = wr0 < p.B;  // wave-uniform
   if (!MZW_PP && !wactive) return;  // (ping-pong: idle waves still meet every slot barrier)
-  MzwWave& ws = wsa[wave];
+  MzwWave<ROOTS>& ws = wsa[wave];
   const double disc = p.discount;
   const bool noised = p.noise != nullptr;
   const size_t E = (size_t)p.E;
@@ -457,7 +444,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 4 * MZW_OCC / MZW_WAVES) void mzh_w
   // root lanes: lane rho < 32 owns root wr0 + rho (tree phases)
   const int rho = lane;
   const int rroot = wr0 + rho;
-  const bool rvalid = lane < MZW_ROOTS && rroot < p.B;
+  const bool rvalid = lane < ROOTS && rroot < p.B;
   MzwBlock* tb = reinterpret_cast<MzwBlock*>(p.tree) + (size_t)(rvalid ? rroot : 0) * E;
   double mmax = -__builtin_inf(), mmin = __builtin_inf();
   if (rvalid && p.minmax_in) {
@@ -470,22 +457,22 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 4 * MZW_OCC / MZW_WAVES) void mzh_w
   const int tie = (rvalid && p.tie_idx) ? p.tie_idx[rroot] : 0;
 
   // column lanes: lane (g, col) works on root wr0 + 16n + col of column tile n (MLP phases)
-  int croot[MZW_NT];
-  bool cvalid[MZW_NT];
+  int croot[NT];
+  bool cvalid[NT];
 #pragma unroll
-  for (int n = 0; n < MZW_NT; ++n) {
+  for (int n = 0; n < NT; ++n) {
     croot[n] = wr0 + 16 * n + col;
     cvalid[n] = croot[n] < p.B;
   }
 
 
   // ---------------- root: initial_inference (mcts.py:49-50) + root.expand (mcts.py:57-69) ----------------
-  floatx4 rpi[MZW_NT];
+  floatx4 rpi[NT];
   if (!REPLAY && wactive) {
-    floatx4 hreg[MZW_NT][4];  // the root's normalised latent (B-operand order)
-    floatx4 x[MZW_NT][4];
+    floatx4 hreg[NT][4];  // the root's normalised latent (B-operand order)
+    floatx4 x[NT][4];
 #pragma unroll
-    for (int n = 0; n < MZW_NT; ++n)
+    for (int n = 0; n < NT; ++n)
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
@@ -493,36 +480,36 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 4 * MZW_OCC / MZW_WAVES) void mzh_w
           const int k = 16 * kb + 4 * t + g;
           x[n][kb][t] = (cvalid[n] && k < p.in_dim) ? p.obs[(size_t)croot[n] * p.in_dim + k] : 0.0f;
         }
-    floatx4 hp[4][MZW_NT];
+    floatx4 hp[4][NT];
     switch (net.rep.kb1) {
-      case 1: mzw_chain<1, 4, false>(net.rep, x, kNoOh, hp, lane); break;
-      case 2: mzw_chain<2, 4, false>(net.rep, x, kNoOh, hp, lane); break;
-      case 3: mzw_chain<3, 4, false>(net.rep, x, kNoOh, hp, lane); break;
-      default: mzw_chain<4, 4, false>(net.rep, x, kNoOh, hp, lane); break;
+      case 1: mzw_chain<NT, 1, 4, false>(net.rep, x, noh, hp, lane); break;
+      case 2: mzw_chain<NT, 2, 4, false>(net.rep, x, noh, hp, lane); break;
+      case 3: mzw_chain<NT, 3, 4, false>(net.rep, x, noh, hp, lane); break;
+      default: mzw_chain<NT, 4, 4, false>(net.rep, x, noh, hp, lane); break;
     }
-    mzw_bias2<4>(net.rep, hp, g);
+    mzw_bias2<NT, 4>(net.rep, hp, g);
 #pragma unroll
-    for (int n = 0; n < MZW_NT; ++n) {
-      mzw_normalize(hp, n, hreg);
+    for (int n = 0; n < NT; ++n) {
+      mzw_normalize<NT>(hp, n, hreg);
       if (cvalid[n]) {
         floatx4* dst = reinterpret_cast<floatx4*>(p.htree + ((size_t)croot[n] * E) * MZH_H) + g;
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) dst[4 * kb] = hreg[n][kb];
       }
     }
-    floatx4 pl[1][MZW_NT];
-    mzw_chain<4, 1, false>(net.pol, hreg, kNoOh, pl, lane);
-    mzw_bias2<1>(net.pol, pl, g);
-    floatx4 vl[NOV][MZW_NT];
-    mzw_chain<4, NOV, false>(net.val, hreg, kNoOh, vl, lane);  // root value: computed, unused (mcts.py:50)
+    floatx4 pl[1][NT];
+    mzw_chain<NT, 4, 1, false>(net.pol, hreg, noh, pl, lane);
+    mzw_bias2<NT, 1>(net.pol, pl, g);
+    floatx4 vl[NOV][NT];
+    mzw_chain<NT, 4, NOV, false>(net.val, hreg, noh, vl, lane);  // root value: computed, unused (mcts.py:50)
     (void)vl;
 #pragma unroll
-    for (int n = 0; n < MZW_NT; ++n) rpi[n] = mzw_policy(pl[0][n], lane);
+    for (int n = 0; n < NT; ++n) rpi[n] = mzw_policy(pl[0][n], lane);
   }
   // root children: prior (Dirichlet-mixed when noised), N = 0, unexpanded
   if (g < 2) {
 #pragma unroll
-    for (int n = 0; n < MZW_NT; ++n)
+    for (int n = 0; n < NT; ++n)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int c = 4 * g + i;
@@ -537,7 +524,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 4 * MZW_OCC / MZW_WAVES) void mzh_w
         }
       }
   }
-  if (lane < MZW_ROOTS) {
+  if (lane < ROOTS) {
 #pragma unroll
     for (int c = 0; c < MZH_A; ++c) {
       ws.rW[c][rho] = 0.0;
@@ -549,18 +536,18 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 4 * MZW_OCC / MZW_WAVES) void mzh_w
   mzw_wave_sync();
 
   // ---- per-simulation phases (shared by both schedules below) ----
-  int en[MZW_NT], an[MZW_NT];    // the leaf's parent (expanded index) and move, per column tile
+  int en[NT], an[NT];    // the leaf's parent (expanded index) and move, per column tile
   // heads: evaluated inside the M phase right after their chain (only scalars stay live), or, in
   // the ping-pong schedule, deferred to the T phase with the logits carried across
   constexpr bool HEADS_IN_M = !MZW_PP;
-  floatx4 rl[NOV][MZW_NT], pl[1][MZW_NT], vl[NOV][MZW_NT];  // reward / policy / value logits
-  float val[MZW_NT], rew[MZW_NT];
-  floatx4 cpi[MZW_NT];
+  floatx4 rl[NOV][NT], pl[1][NT], vl[NOV][NT];  // reward / policy / value logits
+  float val[NT], rew[NT];
+  floatx4 cpi[NT];
 
   // T-phase part 1: select one leaf per root, then gather its parent latent
   auto phase_select = [&](int s) {
     if (MZW_ONLYM) {  // DIAGNOSTIC ONLY: no tree work (the MLP always expands the root's first child)
-      for (int n = 0; n < MZW_NT; ++n) en[n] = an[n] = 0;
+      for (int n = 0; n < NT; ++n) en[n] = an[n] = 0;
       return;
     }
     // ---------------- select (mcts.py:75-86; node.py:72-123): one lane per root ----------------
@@ -655,7 +642,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 4 * MZW_OCC / MZW_WAVES) void mzh_w
     }
     if (!REPLAY) {
 #pragma unroll
-      for (int n = 0; n < MZW_NT; ++n) {
+      for (int n = 0; n < NT; ++n) {
         en[n] = __shfl(leafE, 16 * n + col);
         an[n] = __shfl(leafA, 16 * n + col);
       }
@@ -667,49 +654,49 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 4 * MZW_OCC / MZW_WAVES) void mzh_w
   auto phase_mlp = [&](int s) {
     if (REPLAY) return;
     // the leaf's parent latent (mcts.py:89-92), stored by an earlier M phase (or the root inference)
-    floatx4 x[MZW_NT][4];
+    floatx4 x[NT][4];
 #pragma unroll
-    for (int n = 0; n < MZW_NT; ++n) {
+    for (int n = 0; n < NT; ++n) {
       const floatx4* src = reinterpret_cast<const floatx4*>(p.htree + ((size_t)(cvalid[n] ? croot[n] : 0) * E + en[n]) * MZH_H) + g;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) x[n][kb] = src[4 * kb];
     }
-    floatx4 hreg[MZW_NT][4];  // the new node's normalised latent
-    floatx4 hp[4][MZW_NT];
-    const float* ohp[MZW_NT];
+    floatx4 hreg[NT][4];  // the new node's normalised latent
+    floatx4 hp[4][NT];
+    const float* ohp[NT];
 #pragma unroll
-    for (int n = 0; n < MZW_NT; ++n) ohp[n] = ohl + an[n] * MZH_F + 4 * g;
-    mzw_chain<4, 4, true>(net.dyn, x, ohp, hp, lane);
-    mzw_bias2<4>(net.dyn, hp, g);  // h' (un-normalised, networks.py:129-138)
-    floatx4 hx[MZW_NT][4];
+    for (int n = 0; n < NT; ++n) ohp[n] = ohl + an[n] * MZH_F + 4 * g;
+    mzw_chain<NT, 4, 4, true>(net.dyn, x, ohp, hp, lane);
+    mzw_bias2<NT, 4>(net.dyn, hp, g);  // h' (un-normalised, networks.py:129-138)
+    floatx4 hx[NT][4];
 #pragma unroll
-    for (int n = 0; n < MZW_NT; ++n)
+    for (int n = 0; n < NT; ++n)
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) hx[n][kb] = hp[kb][n];
-    mzw_chain<4, NOV, false>(net.rwd, hx, kNoOh, rl, lane);  // reward from h' (networks.py:132-135)
-    mzw_bias2<NOV>(net.rwd, rl, g);
+    mzw_chain<NT, 4, NOV, false>(net.rwd, hx, noh, rl, lane);  // reward from h' (networks.py:132-135)
+    mzw_bias2<NT, NOV>(net.rwd, rl, g);
     if (HEADS_IN_M)
 #pragma unroll
-      for (int n = 0; n < MZW_NT; ++n) rew[n] = mzw_head<NOV>(rl, n, lane);
+      for (int n = 0; n < NT; ++n) rew[n] = mzw_head<NT, NOV>(rl, n, lane);
 #pragma unroll
-    for (int n = 0; n < MZW_NT; ++n) {
-      mzw_normalize(hp, n, hreg);
+    for (int n = 0; n < NT; ++n) {
+      mzw_normalize<NT>(hp, n, hreg);
       if (cvalid[n]) {
         floatx4* dst = reinterpret_cast<floatx4*>(p.htree + ((size_t)croot[n] * E + s + 1) * MZH_H) + g;
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) dst[4 * kb] = hreg[n][kb];
       }
     }
-    mzw_chain<4, 1, false>(net.pol, hreg, kNoOh, pl, lane);
-    mzw_bias2<1>(net.pol, pl, g);
+    mzw_chain<NT, 4, 1, false>(net.pol, hreg, noh, pl, lane);
+    mzw_bias2<NT, 1>(net.pol, pl, g);
     if (HEADS_IN_M)
 #pragma unroll
-      for (int n = 0; n < MZW_NT; ++n) cpi[n] = mzw_policy(pl[0][n], lane);
-    mzw_chain<4, NOV, false>(net.val, hreg, kNoOh, vl, lane);
-    mzw_bias2<NOV>(net.val, vl, g);
+      for (int n = 0; n < NT; ++n) cpi[n] = mzw_policy(pl[0][n], lane);
+    mzw_chain<NT, 4, NOV, false>(net.val, hreg, noh, vl, lane);
+    mzw_bias2<NT, NOV>(net.val, vl, g);
     if (HEADS_IN_M)
 #pragma unroll
-      for (int n = 0; n < MZW_NT; ++n) val[n] = mzw_head<NOV>(vl, n, lane);
+      for (int n = 0; n < NT; ++n) val[n] = mzw_head<NT, NOV>(vl, n, lane);
   };
 
   // T-phase part 0: heads of simulation s, the new node's block, backup (node.py:30-70)
@@ -718,15 +705,15 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 4 * MZW_OCC / MZW_WAVES) void mzh_w
     if (!REPLAY) {
       if (!HEADS_IN_M)
 #pragma unroll
-        for (int n = 0; n < MZW_NT; ++n) {
-          rew[n] = mzw_head<NOV>(rl, n, lane);
+        for (int n = 0; n < NT; ++n) {
+          rew[n] = mzw_head<NT, NOV>(rl, n, lane);
           cpi[n] = mzw_policy(pl[0][n], lane);
-          val[n] = mzw_head<NOV>(vl, n, lane);
+          val[n] = mzw_head<NT, NOV>(vl, n, lane);
         }
       // the new node's 6 children (node.py:44-49): lane groups 0/1 hold pi[0..3] / pi[4..5]
       if (g < 2) {
 #pragma unroll
-        for (int n = 0; n < MZW_NT; ++n) {
+        for (int n = 0; n < NT; ++n) {
           if (!cvalid[n]) continue;
           MzwBlock* nb = reinterpret_cast<MzwBlock*>(p.tree) + (size_t)croot[n] * E + (s + 1);
 #pragma unroll
@@ -762,7 +749,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 4 * MZW_OCC / MZW_WAVES) void mzh_w
         vv = val[0];
         rr = rew[0];
 #pragma unroll
-        for (int n = 1; n < MZW_NT; ++n)
+        for (int n = 1; n < NT; ++n)
           if ((lane >> 4) == n) {
             vv = val[n];
             rr = rew[n];
@@ -965,24 +952,31 @@ hipError_t mzh_launch_rcp_check(int nmax, int32_t* bad, hipStream_t stream) {
   return hipGetLastError();
 }
 
-size_t mzh_wave_smem_bytes(int S) { return mzw_hdr_bytes(S) + sizeof(MzwWave) * MZW_WAVES; }
+size_t mzh_wave_smem_bytes(int S, int nt) {
+  return mzw_hdr_bytes(S) + (nt == 1 ? sizeof(MzwWave<16>) : sizeof(MzwWave<32>)) * MZW_WAVES;
+}
 
-template <bool REPLAY, bool SUP33>
+template <int NT, bool REPLAY, bool SUP33>
 static hipError_t launch_wave_t(const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream) {
-  const size_t smem = mzh_wave_smem_bytes(p.S);
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mzh_wave_kernel<REPLAY, SUP33>),
+  const size_t smem = mzh_wave_smem_bytes(p.S, NT);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mzh_wave_kernel<NT, REPLAY, SUP33>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
-  const int per_wg = MZW_WAVES * MZW_ROOTS;
+  const int per_wg = MZW_WAVES * 16 * NT;
   const int grid = (p.B + per_wg - 1) / per_wg;
-  hipLaunchKernelGGL((mzh_wave_kernel<REPLAY, SUP33>), dim3(grid), dim3(MZW_WAVES * 64), smem, stream, net, p);
+  hipLaunchKernelGGL((mzh_wave_kernel<NT, REPLAY, SUP33>), dim3(grid), dim3(MZW_WAVES * 64), smem, stream, net, p);
   return hipGetLastError();
 }
 
-hipError_t mzh_launch_wave_search(bool replay, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream) {
+template <int NT>
+static hipError_t launch_wave_nt(bool replay, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream) {
   const bool sup33 = net.support == 33;
-  if (replay) return sup33 ? launch_wave_t<true, true>(net, p, stream) : launch_wave_t<true, false>(net, p, stream);
-  return sup33 ? launch_wave_t<false, true>(net, p, stream) : launch_wave_t<false, false>(net, p, stream);
+  if (replay) return sup33 ? launch_wave_t<NT, true, true>(net, p, stream) : launch_wave_t<NT, true, false>(net, p, stream);
+  return sup33 ? launch_wave_t<NT, false, true>(net, p, stream) : launch_wave_t<NT, false, false>(net, p, stream);
+}
+
+hipError_t mzh_launch_wave_search(int nt, bool replay, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream) {
+  return nt == 1 ? launch_wave_nt<1>(replay, net, p, stream) : launch_wave_nt<2>(replay, net, p, stream);
 }
 
 #ifdef MZH_STAMPS

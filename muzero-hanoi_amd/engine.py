@@ -128,7 +128,7 @@ class Engine:
                kernel=None):
         """Batched search. Tensors must already be on the device (bench: inputs resident in HBM).
         replay = dict(root_pi, pi, reward, value) -> tree-only mode (mzh_search_replay).
-        kernel = None (automatic by batch size) | "coop" | "wave" (both give identical results)."""
+        kernel = None (automatic by batch size) | "coop" | "wave" | "wave16" (all give identical results)."""
         B = int(tie_idx.shape[0])
         if out is None:
             out = self.alloc_search_outputs(B, n_sims)
@@ -149,7 +149,8 @@ class Engine:
         a.temperature = float(temperature)
         a.deterministic = 1 if deterministic else 0
         a.flags = (_lib.MZH_FLAG_NP1_UCB if np1_ucb else 0) | {None: 0, "coop": _lib.MZH_FLAG_KERNEL_COOP,
-                                                               "wave": _lib.MZH_FLAG_KERNEL_WAVE}[kernel]
+                                                               "wave": _lib.MZH_FLAG_KERNEL_WAVE,
+                                                               "wave16": _lib.MZH_FLAG_KERNEL_WAVE16}[kernel]
         a.obs = ptr(dev(obs, torch.float32))
         a.noise = ptr(dev(noise, torch.float64))
         a.tie_idx = ptr(dev(tie_idx, torch.int32))

@@ -143,7 +143,7 @@ def test_mlp_batch_sizes_vs_oracle(mzh, oracle, B):
 
 
 # ------------------------------------------------------------------------------------ search
-KERNELS = ["coop", "wave"]
+KERNELS = ["coop", "wave", "wave16"]
 
 
 def _run_replay_case(mzh, g, kernel=None):
@@ -264,8 +264,9 @@ def test_search_wave_equals_coop_large_batch(mzh, oracle, B, S, n, td):
         o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0,
                        kernel=kernel)
         res[kernel] = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
-    for k in res["coop"]:
-        assert np.array_equal(res["coop"][k], res["wave"][k], equal_nan=True), k
+    for kernel in KERNELS[1:]:
+        for k in res["coop"]:
+            assert np.array_equal(res["coop"][k], res[kernel][k], equal_nan=True), (kernel, k)
     idx = np.r_[0:32, B - 40:B]
     ref = oracle.search(n, S, obs[idx], flat=flat, support=sup, noise=noise[idx], tie_idx=tie[idx],
                         action_u=u[idx], temperature=1.0)

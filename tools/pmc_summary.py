@@ -7,7 +7,7 @@ import os
 import sys
 
 ROOT = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-KERNEL = sys.argv[2] if len(sys.argv) > 2 else "mzh_wave_kernel"  # substring of the dominant kernel
+KERNEL = sys.argv[2] if len(sys.argv) > 2 else "mzh_wave_kernel<2"  # substring of the dominant kernel
 
 
 def newest(pattern):
