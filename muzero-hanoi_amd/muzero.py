@@ -1,0 +1,128 @@
+"""MuZero agent drop-in (reference: Muzero.py:13-323, `Muzero`) -- SURVEY.md section 8f rank 3.
+
+Same constructor and `training_loop(n_loops, min_replay_size, print_acc)` as the reference, so
+`training_main.py` can construct it unchanged.  What runs where on the MI355X:
+  * self-play (`_play_game`): every search is one fused libmzh kernel launch (mcts.MCTS) and the
+    environment step is the reference's (selfplay.play_game);
+  * the replay buffer keeps its transitions on the training device (buffer.Buffer);
+  * the update (`_update`, Muzero.py:209-274): the 5-step unrolled loss of the reference -- the
+    same torch operations in the same order (represent, prediction/dynamics per unroll step,
+    0.5 gradient scaling of the dynamics latent, MSE value / reward and cross-entropy policy terms,
+    importance weights, 1/unroll gradient scaling, Adam) -- on PyTorch-ROCm.  After each update
+    the search engine repacks the weights (networks.engine_for tracks parameter versions).
+"""
+import logging
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .buffer import Buffer
+from .mcts import MCTS
+from .networks import MuZeroNet
+from .selfplay import play_game
+from .utils import organise_transitions
+
+
+class Muzero:
+    def __init__(self, env, s_space_size, n_action, discount, dirichlet_alpha, n_mcts_simulations, unroll_n_steps,
+                 batch_s, TD_return, n_TD_step, lr, buffer_size, priority_replay, device, n_ep_x_loop=1,
+                 n_update_x_loop=1):
+        self.dev = device
+        self.env = env
+        self.n_ep_x_loop = n_ep_x_loop  # episodes collected per training loop
+        self.discount = discount
+        self.n_action = n_action
+        self.unroll_n_steps = unroll_n_steps
+        self.n_update_x_loop = n_update_x_loop  # updates per training loop
+        self.batch_s = batch_s
+        self.TD_return = TD_return
+        self.n_step = n_TD_step
+        self.mcts = MCTS(discount=discount, root_dirichlet_alpha=dirichlet_alpha, n_simulations=n_mcts_simulations,
+                         batch_s=batch_s, device=device)
+        self.networks = MuZeroNet(rpr_input_s=s_space_size, action_s=n_action, lr=lr, TD_return=TD_return,
+                                  device=device).to(device)
+        self.buffer = Buffer(buffer_size, unroll_n_steps, d_state=s_space_size, n_action=n_action, device=device)
+        self.priority_replay = priority_replay
+
+    # ------------------------------------------------------------------ Muzero.py:81-151
+    def training_loop(self, n_loops, min_replay_size, print_acc=50):
+        logging.info("Training started \n")
+        accuracy, tot_accuracy = [], []
+        value_loss, rwd_loss, pi_loss = [], [], []
+        for n in range(1, n_loops):
+            ep_steps = []
+            for _ in range(self.n_ep_x_loop):
+                steps, states, rwds, actions, pi_probs, returns, priorities = self._play_game(
+                    episode=n * self.n_ep_x_loop, deterministic=False)
+                ep_steps.append(steps)
+                if returns[-1, 0] > 0:  # only successful episodes enter the buffer
+                    self.buffer.add(states, rwds, actions, pi_probs, returns, priorities)
+            accuracy.append(sum(ep_steps) / self.n_ep_x_loop)
+            if len(self.buffer) > min_replay_size:
+                for _ in range(self.n_update_x_loop):
+                    if self.priority_replay:
+                        states, rwds, actions, pi_probs, returns, indx, w = self.buffer.priority_sample(self.batch_s)
+                    else:
+                        states, rwds, actions, pi_probs, returns = self.buffer.uniform_sample(self.batch_s)
+                        indx, w = None, None
+                    new_prio, v_loss, r_loss, p_loss = self._update(states, rwds, actions, pi_probs, returns, w)
+                    self.buffer.update_priorities(indx, new_prio)
+                value_loss.append(v_loss)
+                rwd_loss.append(r_loss)
+                pi_loss.append(p_loss)
+            if n * self.n_ep_x_loop % print_acc == 0:
+                mean_acc = sum(accuracy) / print_acc
+                logging.info("Loop %s | steps %.3f | V %.3f | rwd %.3f | Pi %.3f", n, mean_acc,
+                             sum(value_loss) / print_acc, sum(rwd_loss) / print_acc, sum(pi_loss) / print_acc)
+                tot_accuracy.append(mean_acc)
+                accuracy = []
+                value_loss, rwd_loss, pi_loss = [], [], []
+        return tot_accuracy
+
+    # ------------------------------------------------------------------ Muzero.py:153-207
+    def _play_game(self, episode, deterministic=False):
+        return play_game(self.env, self.mcts, self.networks, episode, deterministic, discount=self.discount,
+                         TD_return=self.TD_return, n_step=self.n_step, unroll_n_steps=self.unroll_n_steps,
+                         n_action=self.n_action)
+
+    # ------------------------------------------------------------------ Muzero.py:209-274
+    def _update(self, states, rwds, actions, pi_probs, returns, priority_w):
+        net, U = self.networks, self.unroll_n_steps
+        v_terms, r_terms, p_terms, pred_values_t = unrolled_losses(net, states, rwds, actions, pi_probs, returns, U,
+                                                                    self.dev)
+        loss = v_terms + r_terms + p_terms
+        new_priorities = None
+        if priority_w is not None:
+            loss = loss * priority_w.detach()  # importance-sampling weights of the prioritised sample
+            with torch.no_grad():
+                pred0 = torch.stack(pred_values_t, dim=1).squeeze(-1)[:, 0]
+                new_priorities = (pred0 - returns[:, 0]).abs().cpu().numpy()
+        loss = loss.mean()
+        loss.register_hook(lambda grad: grad * (1 / U))  # loss scaled by 1/unroll_steps (through the hook)
+        net.update(loss)
+        return new_priorities, v_terms.mean().detach(), r_terms.mean().detach(), p_terms.mean().detach()
+
+    def organise_transitions(self, episode_state, episode_rwd, episode_action, episode_piProb, episode_returns):
+        """Muzero.py:276-323"""
+        return organise_transitions(episode_state, episode_rwd, episode_action, episode_piProb, episode_returns,
+                                    self.unroll_n_steps, self.n_action)
+
+
+def unrolled_losses(net, states, rwds, actions, pi_probs, returns, unroll_n_steps, device):
+    """Per-sample value / reward / policy loss sums over the unrolled steps (Muzero.py:213-245), in
+    the reference's operation order: h = represent(s); for each step t: prediction(h), then
+    dynamics(h, onehot(a_t)) with the new latent's gradient halved, then the three loss terms."""
+    v_sum = r_sum = p_sum = 0
+    pred_values_t = []
+    h = net.represent(states)
+    for t in range(unroll_n_steps):
+        pi_logits, values = net.prediction(h)
+        onehot = F.one_hot(actions[:, t], num_classes=net.num_actions).squeeze().to(device, dtype=torch.long)
+        h, pred_rwds = net.dynamics(h, onehot)
+        h.register_hook(lambda grad: grad * 0.5)  # scale the dynamics gradient by 0.5
+        v_sum += F.mse_loss(values.squeeze(), returns[:, t], reduction="none")
+        r_sum += F.mse_loss(pred_rwds.squeeze(), rwds[:, t], reduction="none")
+        p_sum += F.cross_entropy(pi_logits, pi_probs[:, t], reduction="none")  # logits in, softmax inside
+        pred_values_t.append(values)
+    return v_sum, r_sum, p_sum, pred_values_t

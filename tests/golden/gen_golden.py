@@ -16,6 +16,8 @@ Fixtures (see tests/golden/README.md):
   mlp_N{N}_s{seed}.npz    initial/recurrent inference I/O + raw logits (networks.py:71-150)
   replay_<case>.npz       full run_mcts traces: every network call's inputs/outputs, RNG events,
                           final visits / pi / rootQ / action / min-max (MCTS/mcts.py:34-126)
+  training_<case>.npz     Buffer sampling + Muzero._update steps: indices, IS weights, losses,
+                          new priorities, parameters and Adam moments (Muzero.py:209-274, buffer.py)
 """
 import json
 import os
@@ -386,6 +388,68 @@ def gen_checkpoint():
                         **{k: v.numpy() for k, v in net.state_dict().items() if k.startswith(("policy", "rwd"))})
 
 
+def gen_training(name, n, td, priority, updates=3, buffer_size=96, batch_s=24, seed=11, wseed=5, full=True):
+    """Muzero._update (Muzero.py:209-274) + Buffer (buffer.py) of the reference: a buffer filled
+    with seeded synthetic transitions, then `updates` rounds of {sample, _update,
+    update_priorities}; records the sampled indices / IS weights, the three losses, the new
+    priorities and every parameter after each update (and the Adam state at the end)."""
+    from Muzero import Muzero
+
+    env = TowersOfHanoi(N=n, max_steps=200)
+    torch.manual_seed(wseed)
+    mz = Muzero(env=env, s_space_size=3 * n, n_action=6, discount=0.8, dirichlet_alpha=0.25,
+                n_mcts_simulations=5, unroll_n_steps=5, batch_s=batch_s, TD_return=td, n_TD_step=10,
+                lr=0.002, buffer_size=buffer_size, priority_replay=priority, device="cpu")
+    # initial weights: torch.manual_seed(wseed) then the MuZeroNet constructor (the test rebuilds them)
+    g = np.random.default_rng(seed)
+    T = 70  # > buffer_size: exercises the ring wrap-around of Buffer._add
+    st = g.integers(0, 3, (T, n))
+    states = np.zeros((T, 3 * n), np.float32)
+    states[np.arange(T)[:, None], np.arange(n) * 3 + st] = 1
+    rwds = np.where(g.random((T, 5)) < 0.1, 100.0, np.where(g.random((T, 5)) < 0.3, -0.1, 0.0)).astype(np.float32)
+    actions = g.integers(0, 6, (T, 5)).astype(np.int64)
+    pi_probs = g.dirichlet(np.ones(6), size=(T, 5)).astype(np.float32)
+    returns = g.normal(0.0, 20.0, (T, 5)).astype(np.float32)
+    prios = (g.random(T) + 0.05).astype(np.float32)
+    for a, b in ((0, 40), (40, 70), (0, 50)):  # three adds, the last wraps the ring
+        mz.buffer.add(states[a:b], rwds[a:b], actions[a:b], pi_probs[a:b], returns[a:b], prios[a:b])
+    buf0 = dict(b_states=mz.buffer.states.copy(), b_rwds=mz.buffer.rwds.copy(), b_actions=mz.buffer.actions.copy(),
+                b_pi=mz.buffer.pi_probs.copy(), b_returns=mz.buffer.mc_returns.copy(),
+                b_prios=mz.buffer.priorities.copy(), b_ptr=mz.buffer.ptr, b_full=int(mz.buffer.is_full))
+    np.random.seed(seed)
+    rec = {k: [] for k in ("indx", "isw", "v_loss", "r_loss", "p_loss", "new_prio")}
+    params = []
+    for _ in range(updates):
+        if priority:
+            bs, br, ba, bp, bret, indx, w = mz.buffer.priority_sample(batch_s)
+        else:
+            bs, br, ba, bp, bret = mz.buffer.uniform_sample(batch_s)
+            indx, w = None, None
+        newp, vl, rl, pl = mz._update(bs, br, ba, bp, bret, w)
+        mz.buffer.update_priorities(indx, newp)
+        rec["indx"].append(np.full(batch_s, -1) if indx is None else indx)
+        rec["isw"].append(np.zeros(batch_s, np.float32) if w is None else w.numpy())
+        rec["new_prio"].append(np.zeros(batch_s, np.float32) if newp is None else newp)
+        rec["v_loss"].append(float(vl))
+        rec["r_loss"].append(float(rl))
+        rec["p_loss"].append(float(pl))
+        params.append(np.concatenate([v.detach().numpy().reshape(-1) for v in mz.networks.state_dict().values()]))
+    opt_state = mz.networks.optimiser.state_dict()["state"]
+    exp_avg = np.concatenate([opt_state[i]["exp_avg"].numpy().reshape(-1) for i in sorted(opt_state)])
+    exp_avg_sq = np.concatenate([opt_state[i]["exp_avg_sq"].numpy().reshape(-1) for i in sorted(opt_state)])
+    params = np.array(params, np.float64)
+    extra = dict(final_params=params[-1].astype(np.float32), exp_avg=exp_avg, exp_avg_sq=exp_avg_sq) if full else {}
+    np.savez_compressed(
+        os.path.join(HERE, f"training_{name}.npz"), n=n, td=int(td), priority=int(priority), seed=seed, wseed=wseed,
+        batch_s=batch_s, buffer_size=buffer_size, updates=updates, **buf0,
+        **{k: np.array(v) for k, v in rec.items()},
+        param_sum=params.sum(1), param_sumsq=(params ** 2).sum(1), **extra,
+        final_prios=mz.buffer.priorities.copy(), post_rng=np.random.random_sample(4))
+
+
+TRAINING_CASES = [("n3_td_prio", 3, True, True, True), ("n4_mc_uniform", 4, False, False, False)]
+
+
 EPISODE_CASES = [
     ("n3s25_t1", 3, 25, 40, 3, 1, False),
     ("n3s25_t05", 3, 25, 30, 5, 600, False),
@@ -394,6 +458,8 @@ EPISODE_CASES = [
 
 
 def main():
+    for name, n, td, prio, full in TRAINING_CASES:
+        gen_training(name, n, td, prio, full=full)
     gen_checkpoint()
     for name, n, s, ms, seed, ep, det in EPISODE_CASES:
         gen_episode(name, n, s, ms, seed, ep, det)
