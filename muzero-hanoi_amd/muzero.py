@@ -27,7 +27,7 @@ from .utils import organise_transitions
 class Muzero:
     def __init__(self, env, s_space_size, n_action, discount, dirichlet_alpha, n_mcts_simulations, unroll_n_steps,
                  batch_s, TD_return, n_TD_step, lr, buffer_size, priority_replay, device, n_ep_x_loop=1,
-                 n_update_x_loop=1):
+                 n_update_x_loop=1, graph_update=False):
         self.dev = device
         self.env = env
         self.n_ep_x_loop = n_ep_x_loop  # episodes collected per training loop
@@ -44,6 +44,8 @@ class Muzero:
                                   device=device).to(device)
         self.buffer = Buffer(buffer_size, unroll_n_steps, d_state=s_space_size, n_action=n_action, device=device)
         self.priority_replay = priority_replay
+        # opt-in: the whole update (forward, backward, Adam) replayed as one HIP graph (GraphedUpdate)
+        self._graphed = GraphedUpdate(self) if graph_update else None
 
     # ------------------------------------------------------------------ Muzero.py:81-151
     def training_loop(self, n_loops, min_replay_size, print_acc=50):
@@ -88,6 +90,8 @@ class Muzero:
 
     # ------------------------------------------------------------------ Muzero.py:209-274
     def _update(self, states, rwds, actions, pi_probs, returns, priority_w):
+        if self._graphed is not None:
+            return self._graphed(states, rwds, actions, pi_probs, returns, priority_w)
         net, U = self.networks, self.unroll_n_steps
         v_terms, r_terms, p_terms, pred_values_t = unrolled_losses(net, states, rwds, actions, pi_probs, returns, U,
                                                                     self.dev)
@@ -126,3 +130,114 @@ def unrolled_losses(net, states, rwds, actions, pi_probs, returns, unroll_n_step
         p_sum += F.cross_entropy(pi_logits, pi_probs[:, t], reduction="none")  # logits in, softmax inside
         pred_values_t.append(values)
     return v_sum, r_sum, p_sum, pred_values_t
+
+
+class GraphedUpdate:
+    """`Muzero._update` captured once as a HIP graph and replayed per batch.
+
+    At the reference's batch (256 transitions, 5 unroll steps, 256-wide MLPs) one update is a few
+    hundred small kernels, so on the GPU it is bound by launch overhead, not by the GEMMs.  The
+    graph holds the same torch operations as the eager `_update` (same order, same hooks); the
+    only change is Adam's `capturable=True` form (step count and bias corrections kept on the
+    device, so fp32 rather than Python-float step sizes: ulp-level differences).  Inputs are
+    copied into static buffers, so the batch size and the prioritised/uniform choice are fixed
+    at capture time (the first call).  Warm-up iterations run on a snapshot that is restored
+    before capture, so the graph's first replay is the first real update.
+    """
+
+    def __init__(self, mz, warmup=3):
+        if not str(mz.dev).startswith("cuda"):
+            raise RuntimeError("graph_update needs a GPU device")
+        self.mz = mz
+        self.warmup = warmup
+        self.graph = None
+        net = mz.networks
+        old = net.optimiser
+        net.optimiser = opt_like(old, capturable=True, fused=True)
+
+    def _capture(self, states, rwds, actions, pi_probs, returns, priority_w):
+        mz, net, U = self.mz, self.mz.networks, self.mz.unroll_n_steps
+        self.prio = priority_w is not None
+        self.static_in = [t.detach().clone() for t in (states, rwds, actions, pi_probs, returns)]
+        self.static_w = priority_w.detach().clone() if self.prio else None
+        params = [p.detach().clone() for p in net.parameters()]
+        opt_state = copy_opt_state(net.optimiser)
+
+        def body():
+            v, r, p, pred_values_t = unrolled_losses(net, *self.static_in, U, mz.dev)
+            loss = v + r + p
+            newp = None
+            if self.prio:
+                loss = loss * self.static_w
+                with torch.no_grad():
+                    newp = (torch.stack(pred_values_t, dim=1).squeeze(-1)[:, 0] - self.static_in[4][:, 0]).abs()
+            loss = loss.mean()
+            loss.register_hook(lambda grad: grad * (1 / U))
+            loss.backward()
+            net.optimiser.step()
+            return newp, v.mean().detach(), r.mean().detach(), p.mean().detach()
+
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(self.warmup):
+                net.optimiser.zero_grad(set_to_none=True)
+                body()
+        torch.cuda.current_stream().wait_stream(side)
+        with torch.no_grad():  # undo the warm-up updates
+            for q, p0 in zip(net.parameters(), params):
+                q.copy_(p0)
+            restore_opt_state(net.optimiser, opt_state)
+        net.optimiser.zero_grad(set_to_none=True)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = body()
+
+    def __call__(self, states, rwds, actions, pi_probs, returns, priority_w):
+        if self.graph is None:
+            self._capture(states, rwds, actions, pi_probs, returns, priority_w)
+        else:
+            if (priority_w is not None) != self.prio or states.shape != self.static_in[0].shape:
+                raise ValueError("graph_update: batch shape / sampling mode changed after capture")
+            for dst, src in zip(self.static_in, (states, rwds, actions, pi_probs, returns)):
+                dst.copy_(src)
+            if self.prio:
+                self.static_w.copy_(priority_w)
+        self.graph.replay()
+        newp, v, r, p = self.out
+        return (newp.cpu().numpy() if newp is not None else None), v.clone(), r.clone(), p.clone()
+
+
+def opt_like(old, **overrides):
+    """a torch.optim.Adam with `old`'s parameters, hyper-parameters and state, plus `overrides`"""
+    groups = [{k: v for k, v in g.items() if k != "params"} for g in old.param_groups]
+    params = [p for g in old.param_groups for p in g["params"]]
+    d = dict(groups[0])
+    d.update(overrides)
+    new = torch.optim.Adam(params, **{k: d[k] for k in ("lr", "betas", "eps", "weight_decay", "amsgrad",
+                                                        "capturable", "fused") if k in d})
+    st = old.state_dict()
+    if st["state"]:
+        for s in st["state"].values():  # capturable Adam keeps the step count on the parameter's device
+            s["step"] = torch.as_tensor(float(s["step"]), dtype=torch.float32, device=params[0].device)
+        st["param_groups"][0].update(overrides)
+        new.load_state_dict(st)
+    return new
+
+
+def copy_opt_state(o):
+    return {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in s.items()} for p, s in o.state.items()}
+
+
+def restore_opt_state(o, saved):
+    for p in list(o.state.keys()):
+        if id(p) in saved:
+            for k, v in saved[id(p)].items():
+                if torch.is_tensor(o.state[p][k]) and torch.is_tensor(v):
+                    o.state[p][k].copy_(v)
+                else:
+                    o.state[p][k] = v
+        else:  # state created by the warm-up only: back to "no step taken yet", in place
+            for k, v in o.state[p].items():
+                if torch.is_tensor(v):
+                    v.zero_()
