@@ -160,6 +160,49 @@ int mzh_search(mzh_engine* eng, const mzh_search_args* args, mzh_stream stream);
 int mzh_search_replay(mzh_engine* eng, const mzh_search_args* args, mzh_stream stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * Fused training update.  Replaces Muzero._update (Muzero.py:209-274: represent, U unrolled
+ * prediction/dynamics steps, MSE value/reward and soft-target cross-entropy policy terms, the 0.5
+ * latent-gradient hook, importance weights, the 1/U loss hook) and MuZeroNet.update's Adam step
+ * (networks.py:69,118-122) for one sampled batch, in two kernel launches.
+ *   B, U, in_dim, support : batch_s, unroll_n_steps, 3N, 33 (TD_return) or 1
+ *   rows                  : transitions per workgroup of the row kernel (1, 2 or 4; 0 = auto)
+ *   step_size, bc2_sqrt   : torch.optim.Adam's lr / (1 - beta1^step) and sqrt(1 - beta2^step) for
+ *                           this step (computed by the host in fp64, as torch does); beta1, beta2, eps
+ *   obs [B][in_dim] f32, rwds [B][U] f32, actions [B][U] i64, pi [B][U][6] f32, returns [B][U] f32,
+ *   weights [B] f32 importance weights or NULL (uniform replay)
+ *   param / exp_avg / exp_avg_sq : the 20 MuZeroNet parameters in state_dict order
+ *                           ({representation,dynamic,rwd,policy,value}_net.{0,2}.{weight,bias}) and
+ *                           their Adam moments, updated in place
+ *   wt[10]                : transposed copies [in][out] of the ten weights (param 0,2,...,18), filled
+ *                           by mzh_train_transpose and kept current by mzh_train_update
+ *   scratch               : device workspace of mzh_train_scratch_bytes
+ *   row_loss [B][3]       : per-transition value, reward and policy loss sums (their means are the
+ *                           reference's returned losses); new_prio [B] = |v_0 - return_0| or NULL
+ * ------------------------------------------------------------------------------------------- */
+typedef struct mzh_train_args {
+  int32_t B, U, in_dim, support, rows;
+  float step_size, bc2_sqrt, beta1, beta2, eps;
+  const float* obs;
+  const float* rwds;
+  const int64_t* actions;
+  const float* pi;
+  const float* returns;
+  const float* weights;
+  float* param[20];
+  float* exp_avg[20];
+  float* exp_avg_sq[20];
+  float* wt[10];
+  void* scratch;
+  size_t scratch_bytes;
+  float* row_loss;
+  float* new_prio;
+} mzh_train_args;
+
+int mzh_train_scratch_bytes(int B, int U, int in_dim, int support, size_t* bytes);
+int mzh_train_transpose(const mzh_train_args* args, mzh_stream stream);
+int mzh_train_update(const mzh_train_args* args, mzh_stream stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Device self-tests of numerical building blocks the kernels rely on (no reference equivalent;
  * used by tests/test_gpu_parity.py).  Adds the number of failures to *result (device int32).
  *   MZH_SELFTEST_RCP: the search kernels' register reciprocal RN(1/n) equals IEEE 1.0 / n for

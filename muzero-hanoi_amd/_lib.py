@@ -41,6 +41,18 @@ class SearchArgs(ctypes.Structure):
     ]
 
 
+class TrainArgs(ctypes.Structure):
+    """mirror of struct mzh_train_args (include/mzh.h)"""
+    _f32 = ctypes.c_float
+    _fields_ = [
+        ("B", _i32), ("U", _i32), ("in_dim", _i32), ("support", _i32), ("rows", _i32),
+        ("step_size", _f32), ("bc2_sqrt", _f32), ("beta1", _f32), ("beta2", _f32), ("eps", _f32),
+        ("obs", _vp), ("rwds", _vp), ("actions", _vp), ("pi", _vp), ("returns", _vp), ("weights", _vp),
+        ("param", _vp * 20), ("exp_avg", _vp * 20), ("exp_avg_sq", _vp * 20), ("wt", _vp * 10),
+        ("scratch", _vp), ("scratch_bytes", ctypes.c_size_t), ("row_loss", _vp), ("new_prio", _vp),
+    ]
+
+
 # name -> (restype, argtypes); every symbol include/mzh.h declares
 SIGNATURES = {
     "mzh_abi_version": (ctypes.c_int, []),
@@ -60,6 +72,9 @@ SIGNATURES = {
     "mzh_search": (ctypes.c_int, [_vp, ctypes.POINTER(SearchArgs), _vp]),
     "mzh_search_replay": (ctypes.c_int, [_vp, ctypes.POINTER(SearchArgs), _vp]),
     "mzh_selftest": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _vp]),
+    "mzh_train_scratch_bytes": (ctypes.c_int, [ctypes.c_int] * 4 + [ctypes.POINTER(ctypes.c_size_t)]),
+    "mzh_train_transpose": (ctypes.c_int, [ctypes.POINTER(TrainArgs), _vp]),
+    "mzh_train_update": (ctypes.c_int, [ctypes.POINTER(TrainArgs), _vp]),
 }
 
 _lib = None

@@ -15,7 +15,7 @@ CSRC = os.path.join(HERE, "csrc")
 REPO = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libmzh.so")
 OBJ = os.path.join(HERE, "_obj")
-SOURCES = ["mzh_api.hip", "mzh_search.hip", "mzh_wave.hip", "mzh_env.hip"]
+SOURCES = ["mzh_api.hip", "mzh_search.hip", "mzh_wave.hip", "mzh_env.hip", "mzh_train.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MZH_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off",

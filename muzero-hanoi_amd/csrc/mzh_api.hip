@@ -12,6 +12,7 @@
 #include "../../include/mzh.h"
 #include "mzh_env_kernels.h"
 #include "mzh_internal.h"
+#include "mzh_train.h"
 
 static thread_local std::string g_err;
 
@@ -486,4 +487,163 @@ extern "C" int mzh_selftest(int test, int n, int32_t* result, mzh_stream stream)
 
 extern "C" int mzh_search_replay(mzh_engine* eng, const mzh_search_args* args, mzh_stream stream) {
   return search_common(eng, args, stream, true);
+}
+
+// ---------------------------------------------------------------------------------------------
+// fused training update (mzh_train.hip)
+namespace {
+struct TrainLayout {
+  size_t off[22];
+  size_t total;  // floats
+};
+// scratch regions in MztScratch order, each 256-B aligned
+TrainLayout train_layout(int B, int U, int support) {
+  const size_t BU = (size_t)B * U, ldg = support > 1 ? 48 : 16;
+  const size_t sz[] = {(size_t)B * 32, (size_t)B * 256, BU * 64, BU * 256, BU * 256, BU * 256, BU * 256, BU * 64,
+                       (size_t)B * 256, (size_t)B * 64, BU * 256, BU * 256, BU * 256, BU * 256, BU * 16, BU * ldg,
+                       BU * ldg, BU * 64};
+  TrainLayout L{};
+  size_t o = 0;
+  for (int i = 0; i < 18; ++i) {
+    L.off[i] = o;
+    o += (sz[i] + 63) & ~(size_t)63;
+  }
+  L.total = o;
+  return L;
+}
+int train_rows(const mzh_train_args* a) {
+  if (a->rows > 0) return a->rows;
+  const char* env = getenv("MZH_TRAIN_ROWS");
+  if (env) return atoi(env);
+  return 1;  // one transition per workgroup: B workgroups (fastest at batch 256, MI355X)
+}
+}  // namespace
+
+extern "C" int mzh_train_scratch_bytes(int B, int U, int in_dim, int support, size_t* bytes) {
+  if (B < 1 || U < 1 || in_dim < 1 || in_dim > 32 || (support != 1 && support != 33) || !bytes)
+    return fail(MZH_ERR_ARG, "train_scratch_bytes: bad B=%d U=%d in_dim=%d support=%d", B, U, in_dim, support);
+  *bytes = train_layout(B, U, support).total * sizeof(float);
+  return MZH_OK;
+}
+
+static int train_check(const mzh_train_args* a, bool need_batch) {
+  if (!a) return fail(MZH_ERR_ARG, "train: null args");
+  if (a->B < 1 || a->U < 1 || a->in_dim < 1 || a->in_dim > 32 || (a->support != 1 && a->support != 33))
+    return fail(MZH_ERR_ARG, "train: bad B=%d U=%d in_dim=%d support=%d", a->B, a->U, a->in_dim, a->support);
+  for (int i = 0; i < 20; ++i)
+    if (!a->param[i] || (need_batch && (!a->exp_avg[i] || !a->exp_avg_sq[i])))
+      return fail(MZH_ERR_ARG, "train: null parameter / Adam state pointer %d", i);
+  for (int i = 0; i < 10; ++i)
+    if (!a->wt[i]) return fail(MZH_ERR_ARG, "train: null transposed weight %d", i);
+  if (!need_batch) return MZH_OK;
+  if (!a->obs || !a->rwds || !a->actions || !a->pi || !a->returns || !a->row_loss || !a->scratch)
+    return fail(MZH_ERR_ARG, "train: null batch / output / scratch pointer");
+  if (a->scratch_bytes < train_layout(a->B, a->U, a->support).total * sizeof(float))
+    return fail(MZH_ERR_ARG, "train: scratch of %zu bytes is too small", a->scratch_bytes);
+  const int R = train_rows(a);
+  if (R != 1 && R != 2 && R != 4) return fail(MZH_ERR_ARG, "train: rows must be 1, 2 or 4 (got %d)", R);
+  if (R * a->U > 64) return fail(MZH_ERR_ARG, "train: rows * U = %d exceeds 64", R * a->U);
+  if (mzt_rows_smem_bytes(R, a->U) > 160 * 1024)
+    return fail(MZH_ERR_ARG, "train: U=%d needs %zu B of LDS at rows=%d", a->U, mzt_rows_smem_bytes(R, a->U), R);
+  return MZH_OK;
+}
+
+// [out, in] of the ten Linear layers in state_dict order (representation layer 1: in = in_dim;
+// value / reward layer 2: out = support)
+static void layer_dims(const mzh_train_args* a, int l, int* out, int* in) {
+  static const int kOut[10] = {256, 64, 256, 64, 256, -1, 256, 6, 256, -1};
+  static const int kIn[10] = {-1, 256, 70, 256, 64, 256, 64, 256, 64, 256};
+  *out = kOut[l] < 0 ? a->support : kOut[l];
+  *in = kIn[l] < 0 ? a->in_dim : kIn[l];
+}
+
+extern "C" int mzh_train_transpose(const mzh_train_args* a, mzh_stream stream) {
+  int st = train_check(a, false);
+  if (st) return st;
+  for (int l = 0; l < 10; ++l) {
+    int out, in;
+    layer_dims(a, l, &out, &in);
+    hipError_t e = mzt_launch_transpose(a->param[2 * l], a->wt[l], out, in, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "train transpose launch");
+  }
+  return MZH_OK;
+}
+
+extern "C" int mzh_train_update(const mzh_train_args* a, mzh_stream stream) {
+  int st = train_check(a, true);
+  if (st) return st;
+  const int B = a->B, U = a->U, SUP = a->support;
+  const TrainLayout lay = train_layout(B, U, SUP);
+  float* base = (float*)a->scratch;
+  MztScratch s;
+  float** regions[] = {&s.x0, &s.repa, &s.h, &s.ap, &s.av, &s.ad, &s.ar, &s.hp, &s.g_rep, &s.g_h0p,
+                       &s.g_p, &s.g_v, &s.g_d, &s.g_r, &s.g_lp, &s.g_lv, &s.g_lr, &s.g_hp};
+  for (int i = 0; i < 18; ++i) *regions[i] = base + lay.off[i];
+
+  float* const* P = a->param;
+  MztRowParams rp;
+  rp.B = B;
+  rp.U = U;
+  rp.in_dim = a->in_dim;
+  rp.obs = a->obs;
+  rp.rwds = a->rwds;
+  rp.pi = a->pi;
+  rp.returns = a->returns;
+  rp.w = a->weights;
+  rp.actions = a->actions;
+  rp.row_loss = a->row_loss;
+  rp.new_prio = a->new_prio;
+  float* const* T = a->wt;
+  rp.n = MztNet{P[0],  T[0], P[1],  P[2],  T[1], P[3],  P[4],  T[2], P[5],  P[6],  T[3], P[7],
+                P[8],  T[4], P[9],  P[10], T[5], P[11], P[12], T[6], P[13], P[14], T[7], P[15],
+                P[16], T[8], P[17], P[18], T[9], P[19]};
+  rp.s = s;
+  hipError_t e = mzt_launch_rows(train_rows(a), SUP, rp, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "train rows kernel launch");
+
+  const int BU = B * U, ldg = SUP > 1 ? 48 : 16;
+  struct Spec {
+    const float* X;
+    int ldx;
+    const float* GY;
+    int ldg, M, out, in, onehot;
+  };
+  const Spec spec[10] = {
+      {s.x0, 32, s.g_rep, 256, B, 256, a->in_dim, -1}, {s.repa, 256, s.g_h0p, 64, B, 64, 256, -1},
+      {s.h, 64, s.g_d, 256, BU, 256, 70, 64},          {s.ad, 256, s.g_hp, 64, BU, 64, 256, -1},
+      {s.hp, 64, s.g_r, 256, BU, 256, 64, -1},         {s.ar, 256, s.g_lr, ldg, BU, SUP, 256, -1},
+      {s.h, 64, s.g_p, 256, BU, 256, 64, -1},          {s.ap, 256, s.g_lp, 16, BU, 6, 256, -1},
+      {s.h, 64, s.g_v, 256, BU, 256, 64, -1},          {s.av, 256, s.g_lv, ldg, BU, SUP, 256, -1}};
+  MztGradParams gp;
+  int tiles = 0;
+  for (int l = 0; l < 10; ++l) {
+    MztGradLayer& L = gp.L[l];
+    const Spec& q = spec[l];
+    L.X = q.X;
+    L.ldx = q.ldx;
+    L.GY = q.GY;
+    L.ldg = q.ldg;
+    L.M = q.M;
+    L.out = q.out;
+    L.in = q.in;
+    L.onehot_from = q.onehot;
+    L.nkb = (q.in + 15) / 16;
+    L.tile0 = tiles;
+    tiles += ((q.out + 15) / 16) * L.nkb;
+    L.W = a->param[2 * l];
+    L.b = a->param[2 * l + 1];
+    L.mW = a->exp_avg[2 * l];
+    L.vW = a->exp_avg_sq[2 * l];
+    L.mb = a->exp_avg[2 * l + 1];
+    L.vb = a->exp_avg_sq[2 * l + 1];
+    L.WT = a->wt[l];
+  }
+  gp.actions = a->actions;
+  gp.step_size = a->step_size;
+  gp.bc2_sqrt = a->bc2_sqrt;
+  gp.beta1 = a->beta1;
+  gp.beta2 = a->beta2;
+  gp.eps = a->eps;
+  e = mzt_launch_grad_adam(gp, tiles, (hipStream_t)stream);
+  return e == hipSuccess ? MZH_OK : hip_fail(e, "train grad/adam kernel launch");
 }

@@ -11,11 +11,14 @@ Same constructor and `training_loop(n_loops, min_replay_size, print_acc)` as the
     importance weights, 1/unroll gradient scaling, Adam) -- on PyTorch-ROCm.  After each update
     the search engine repacks the weights (networks.engine_for tracks parameter versions).
 """
+import ctypes
 import logging
+import math
 
 import numpy as np
 import torch
 import torch.nn.functional as F
+from torch.autograd.graph import increment_version
 
 from .buffer import Buffer
 from .mcts import MCTS
@@ -27,7 +30,7 @@ from .utils import organise_transitions
 class Muzero:
     def __init__(self, env, s_space_size, n_action, discount, dirichlet_alpha, n_mcts_simulations, unroll_n_steps,
                  batch_s, TD_return, n_TD_step, lr, buffer_size, priority_replay, device, n_ep_x_loop=1,
-                 n_update_x_loop=1, graph_update=False):
+                 n_update_x_loop=1, update_impl="torch"):
         self.dev = device
         self.env = env
         self.n_ep_x_loop = n_ep_x_loop  # episodes collected per training loop
@@ -44,8 +47,14 @@ class Muzero:
                                   device=device).to(device)
         self.buffer = Buffer(buffer_size, unroll_n_steps, d_state=s_space_size, n_action=n_action, device=device)
         self.priority_replay = priority_replay
-        # opt-in: the whole update (forward, backward, Adam) replayed as one HIP graph (GraphedUpdate)
-        self._graphed = GraphedUpdate(self) if graph_update else None
+        # update_impl (not in the reference's signature): "torch" = the reference's op sequence,
+        # "graph" = that sequence replayed as one HIP graph (GraphedUpdate), "fused" = the two-kernel
+        # HIP update of libmzh (FusedUpdate)
+        if update_impl not in ("torch", "graph", "fused"):
+            raise ValueError(f"update_impl must be 'torch', 'graph' or 'fused', not {update_impl!r}")
+        self._graphed = {"torch": None, "graph": GraphedUpdate, "fused": FusedUpdate}[update_impl]
+        if self._graphed is not None:
+            self._graphed = self._graphed(self)
 
     # ------------------------------------------------------------------ Muzero.py:81-151
     def training_loop(self, n_loops, min_replay_size, print_acc=50):
@@ -241,3 +250,104 @@ def restore_opt_state(o, saved):
             for k, v in o.state[p].items():
                 if torch.is_tensor(v):
                     v.zero_()
+
+
+class FusedUpdate:
+    """`Muzero._update` + Adam as libmzh's fused HIP training update (csrc/mzh_train.hip).
+
+    Launch 1 runs, per transition, the U-step unrolled forward and the complete backward pass of
+    the reference's loss (Muzero.py:213-265) in one workgroup; launch 2 forms every weight gradient
+    as a GEMM over the B*U rows on fp32 MFMA and applies torch.optim.Adam's update in place on the
+    module's parameters and the optimiser's own state tensors, so `networks.state_dict()` and
+    `networks.optimiser.state_dict()` (the checkpoint of training_main.py:93-103) stay the
+    reference's.  Adam's step counter and bias corrections are the host-side Python floats torch
+    uses.  Results match the torch update to fp32 rounding (other summation orders).
+    """
+
+    def __init__(self, mz):
+        if not str(mz.dev).startswith("cuda"):
+            raise RuntimeError("update_impl='fused' needs a GPU device")
+        from . import _lib
+        self._lib = _lib
+        self.mz = mz
+        net = mz.networks
+        self.params = list(net.parameters())
+        if len(self.params) != 20:
+            raise ValueError("fused update expects MuZeroNet's 20 parameter tensors")
+        g = net.optimiser.param_groups[0]
+        if not isinstance(net.optimiser, torch.optim.Adam) or g["weight_decay"] != 0 or g["amsgrad"] \
+                or g.get("maximize", False) or len(net.optimiser.param_groups) != 1:
+            raise ValueError("fused update implements plain torch.optim.Adam (no weight decay / amsgrad)")
+        self.support = net.support_size
+        self.in_dim = self.params[0].shape[1]
+        dev = self.params[0].device
+        self.wt = [torch.empty(p.shape[1], p.shape[0], dtype=torch.float32, device=dev) for p in self.params[0::2]]
+        self.scratch = None
+        self.B = None
+        self._seen = None  # parameter versions after our own last write
+
+    def _versions(self):
+        return tuple((p.data_ptr(), p._version) for p in self.params)
+
+    def _state(self):
+        opt = self.mz.networks.optimiser
+        for p in self.params:
+            st = opt.state[p]
+            if len(st) == 0:  # torch.optim.Adam._init_group's lazy state
+                st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        return [opt.state[p] for p in self.params]
+
+    def _args(self, B):
+        L = self._lib
+        a = L.TrainArgs()
+        a.B, a.U, a.in_dim, a.support, a.rows = B, self.mz.unroll_n_steps, self.in_dim, self.support, 0
+        for i, p in enumerate(self.params):
+            a.param[i] = p.data_ptr()
+        for i, w in enumerate(self.wt):
+            a.wt[i] = w.data_ptr()
+        return a
+
+    def __call__(self, states, rwds, actions, pi_probs, returns, priority_w):
+        L = self._lib
+        B, U = states.shape[0], self.mz.unroll_n_steps
+        stream = torch.cuda.current_stream().cuda_stream
+        if self.B != B:
+            nb = ctypes.c_size_t()
+            L.check(L.lib().mzh_train_scratch_bytes(B, U, self.in_dim, self.support, nb), "mzh_train_scratch_bytes")
+            self.scratch = torch.empty(nb.value // 4 + 64, dtype=torch.float32, device=states.device)
+            self.row_loss = torch.empty(B, 3, dtype=torch.float32, device=states.device)
+            self.new_prio = torch.empty(B, dtype=torch.float32, device=states.device)
+            self.B = B
+        a = self._args(B)
+        if self._seen != self._versions():  # parameters written outside this update: re-transpose
+            L.check(L.lib().mzh_train_transpose(a, stream), "mzh_train_transpose")
+        states_ = self._state()
+        g = self.mz.networks.optimiser.param_groups[0]
+        beta1, beta2 = g["betas"]
+        for st in states_:
+            st["step"] += 1
+        step = float(states_[0]["step"])
+        a.step_size = g["lr"] / (1 - beta1 ** step)
+        a.bc2_sqrt = math.sqrt(1 - beta2 ** step)
+        a.beta1, a.beta2, a.eps = beta1, beta2, g["eps"]
+        for i, st in enumerate(states_):
+            a.exp_avg[i] = st["exp_avg"].data_ptr()
+            a.exp_avg_sq[i] = st["exp_avg_sq"].data_ptr()
+        ins = [states.float().contiguous(), rwds.float().contiguous(), actions.long().contiguous(),
+               pi_probs.float().contiguous(), returns.float().contiguous()]
+        w = priority_w.float().contiguous() if priority_w is not None else None
+        a.obs, a.rwds, a.actions, a.pi, a.returns = (t.data_ptr() for t in ins)
+        a.weights = w.data_ptr() if w is not None else None
+        a.scratch = self.scratch.data_ptr()
+        a.scratch_bytes = self.scratch.numel() * 4
+        a.row_loss = self.row_loss.data_ptr()
+        a.new_prio = self.new_prio.data_ptr() if w is not None else None
+        L.check(L.lib().mzh_train_update(a, stream), "mzh_train_update")
+        for p in self.params:  # the kernel wrote the parameters in place: let version trackers know
+            increment_version(p)
+        self._seen = self._versions()
+        means = self.row_loss.mean(0)
+        newp = self.new_prio.cpu().numpy() if w is not None else None
+        return newp, means[0], means[1], means[2]

@@ -42,8 +42,31 @@ def test_search_args_layout_matches_header(lib):
     # the C struct: 2 x int32, 3 x double, int32, uint32, 18 pointers
     assert ctypes.sizeof(lib.SearchArgs) == 8 + 24 + 8 + 18 * 8
     assert lib.SearchArgs.obs.offset == 40
-    n_ptr_fields = len(re.findall(r"^\s+(?:const\s+)?\w+\*\s+\w+;", open(HEADER).read(), re.M))
+    hdr = open(HEADER).read()
+    block = hdr[hdr.index("typedef struct mzh_search_args"):]
+    block = block[:block.index("} mzh_search_args;")]
+    n_ptr_fields = len(re.findall(r"^\s+(?:const\s+)?\w+\*\s+\w+;", block, re.M))
     assert n_ptr_fields == 18
+
+
+def test_train_args_layout_matches_header(lib, tmp_path):
+    """ctypes TrainArgs == struct mzh_train_args as the C compiler lays it out"""
+    import shutil
+    import subprocess
+
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    fields = [f[0] for f in lib.TrainArgs._fields_]
+    src = tmp_path / "off.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "mzh.h"\nint main(void){\n'
+                   + "".join(f'printf("%zu\\n", offsetof(mzh_train_args, {f}));\n' for f in fields)
+                   + 'printf("%zu\\n", sizeof(mzh_train_args)); return 0; }\n')
+    exe = tmp_path / "off"
+    subprocess.run([cc, "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    want = [getattr(lib.TrainArgs, f).offset for f in fields] + [ctypes.sizeof(lib.TrainArgs)]
+    assert got == want
 
 
 def test_errors_without_device_are_loud(lib):

@@ -29,7 +29,7 @@ def synthetic_transitions(n, seed, T=70):
     return states, rwds, actions, pi_probs, returns, prios
 
 
-def run_case(g, device, graph=False):
+def run_case(g, device, impl="torch"):
     from muzero_hanoi_amd.muzero import Muzero
 
     n, td, prio = int(g["n"]), bool(g["td"]), bool(g["priority"])
@@ -37,7 +37,7 @@ def run_case(g, device, graph=False):
     mz = Muzero(env=None, s_space_size=3 * n, n_action=6, discount=0.8,
                 dirichlet_alpha=0.25, n_mcts_simulations=5, unroll_n_steps=5, batch_s=int(g["batch_s"]), TD_return=td,
                 n_TD_step=10, lr=0.002, buffer_size=int(g["buffer_size"]), priority_replay=prio, device=device,
-                graph_update=graph)
+                update_impl=impl)
     data = synthetic_transitions(n, int(g["seed"]))
     for a, b in ((0, 40), (40, 70), (0, 50)):
         mz.buffer.add(*(x[a:b] for x in data))
@@ -96,14 +96,14 @@ def test_buffer_and_update_vs_reference_on_cpu(case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
+@pytest.mark.parametrize("impl", ["torch", "graph", "fused"])
 @pytest.mark.parametrize("case", CASES)
-def test_update_on_gpu_vs_reference(case, graph):
+def test_update_on_gpu_vs_reference(case, impl):
     """PyTorch-ROCm update vs the reference's CPU update: same samples, losses and priorities to
     fp32 reduction-order tolerance; parameters after 3 Adam steps within a few lr of each other
     only where a gradient sits at the rounding noise (Adam's first steps move by ~lr * sign(g))."""
     g = golden(f"training_{case}.npz")
-    out = run_case(g, "cuda", graph=graph)
+    out = run_case(g, "cuda", impl=impl)
     for k in ("indx", "post_rng"):
         assert np.array_equal(np.array(out[k]), g[k]), k
     np.testing.assert_allclose(np.array(out["isw"]), g["isw"], rtol=1e-6)

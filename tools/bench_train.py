@@ -3,9 +3,10 @@
 at the reference's TrainingConfig (training_main.py:15-34: Hanoi N=3, batch 256, 5 unroll steps,
 TD returns, prioritised replay, buffer 50,000, lr 0.002), on synthetic transitions filling the
 buffer.  Legs: the update on the host CPU (the reference's torch op sequence, parity-tested
-against the reference's own fixtures), the eager update on the GPU, and the HIP-graph update.
+against the reference's own fixtures), the eager update on the GPU, the HIP-graph update, and the
+fused two-kernel HIP update (csrc/mzh_train.hip).
 
-  python tools/bench_train.py [--legs cpu,gpu,graph] [--steps K] [--warmup W] [--batch 256]
+  python tools/bench_train.py [--legs cpu,gpu,graph,fused] [--steps K] [--warmup W] [--batch 256]
 
 Prints one JSON line per leg: updates/s, samples/s (= transitions consumed per second) and
 ms per update, plus the update-only time (sampling excluded).
@@ -51,7 +52,8 @@ def run_leg(leg, args):
     n = args.disks
     mz = Muzero(env=None, s_space_size=3 * n, n_action=6, discount=0.8, dirichlet_alpha=0.25, n_mcts_simulations=25,
                 unroll_n_steps=5, batch_s=args.batch, TD_return=True, n_TD_step=10, lr=0.002,
-                buffer_size=args.buffer, priority_replay=True, device=dev, graph_update=(leg == "graph"))
+                buffer_size=args.buffer, priority_replay=True, device=dev,
+                update_impl={"cpu": "torch", "gpu": "torch"}.get(leg, leg))
     synthetic_fill(mz, n, args.buffer)
     buf = mz.buffer
     sync = torch.cuda.synchronize if dev == "cuda" else (lambda: None)
@@ -92,7 +94,7 @@ def run_leg(leg, args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--legs", default="cpu,gpu,graph")
+    ap.add_argument("--legs", default="cpu,gpu,graph,fused")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--cpu-steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
