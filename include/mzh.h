@@ -165,7 +165,7 @@ int mzh_search_replay(mzh_engine* eng, const mzh_search_args* args, mzh_stream s
  * latent-gradient hook, importance weights, the 1/U loss hook) and MuZeroNet.update's Adam step
  * (networks.py:69,118-122) for one sampled batch, in two kernel launches.
  *   B, U, in_dim, support : batch_s, unroll_n_steps, 3N, 33 (TD_return) or 1
- *   rows                  : transitions per workgroup of the row kernel (1, 2 or 4; 0 = auto)
+ *   rows                  : transitions per workgroup of the row kernel (1 or 2; 0 = auto)
  *   step_size, bc2_sqrt   : torch.optim.Adam's lr / (1 - beta1^step) and sqrt(1 - beta2^step) for
  *                           this step (computed by the host in fp64, as torch does); beta1, beta2, eps
  *   obs [B][in_dim] f32, rwds [B][U] f32, actions [B][U] i64, pi [B][U][6] f32, returns [B][U] f32,
@@ -173,8 +173,9 @@ int mzh_search_replay(mzh_engine* eng, const mzh_search_args* args, mzh_stream s
  *   param / exp_avg / exp_avg_sq : the 20 MuZeroNet parameters in state_dict order
  *                           ({representation,dynamic,rwd,policy,value}_net.{0,2}.{weight,bias}) and
  *                           their Adam moments, updated in place
- *   wt[10]                : transposed copies [in][out] of the ten weights (param 0,2,...,18), filled
- *                           by mzh_train_transpose and kept current by mzh_train_update
+ *   wt[10]                : transposed copies [in][round_up(out, 4)] of the ten weights (param
+ *                           0,2,...,18; pad columns zero), filled by mzh_train_transpose and kept
+ *                           current by mzh_train_update
  *   scratch               : device workspace of mzh_train_scratch_bytes
  *   row_loss [B][3]       : per-transition value, reward and policy loss sums (their means are the
  *                           reference's returned losses); new_prio [B] = |v_0 - return_0| or NULL

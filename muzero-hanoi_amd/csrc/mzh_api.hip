@@ -541,7 +541,7 @@ static int train_check(const mzh_train_args* a, bool need_batch) {
   if (a->scratch_bytes < train_layout(a->B, a->U, a->support).total * sizeof(float))
     return fail(MZH_ERR_ARG, "train: scratch of %zu bytes is too small", a->scratch_bytes);
   const int R = train_rows(a);
-  if (R != 1 && R != 2 && R != 4) return fail(MZH_ERR_ARG, "train: rows must be 1, 2 or 4 (got %d)", R);
+  if (R != 1 && R != 2) return fail(MZH_ERR_ARG, "train: rows must be 1 or 2 (got %d)", R);
   if (R * a->U > 64) return fail(MZH_ERR_ARG, "train: rows * U = %d exceeds 64", R * a->U);
   if (mzt_rows_smem_bytes(R, a->U) > 160 * 1024)
     return fail(MZH_ERR_ARG, "train: U=%d needs %zu B of LDS at rows=%d", a->U, mzt_rows_smem_bytes(R, a->U), R);
@@ -563,7 +563,7 @@ extern "C" int mzh_train_transpose(const mzh_train_args* a, mzh_stream stream) {
   for (int l = 0; l < 10; ++l) {
     int out, in;
     layer_dims(a, l, &out, &in);
-    hipError_t e = mzt_launch_transpose(a->param[2 * l], a->wt[l], out, in, (hipStream_t)stream);
+    hipError_t e = mzt_launch_transpose(a->param[2 * l], a->wt[l], out, in, (out + 3) & ~3, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "train transpose launch");
   }
   return MZH_OK;
@@ -637,6 +637,7 @@ extern "C" int mzh_train_update(const mzh_train_args* a, mzh_stream stream) {
     L.mb = a->exp_avg[2 * l + 1];
     L.vb = a->exp_avg_sq[2 * l + 1];
     L.WT = a->wt[l];
+    L.ldwt = (q.out + 3) & ~3;
   }
   gp.actions = a->actions;
   gp.step_size = a->step_size;

@@ -49,7 +49,8 @@ struct MztGradLayer {
   int onehot_from;  // columns >= onehot_from are the one-hot action (dynamics layer 1), else -1
   int tile0, nkb;   // first tile of this layer in the grid, 16-column blocks of `in`
   float *W, *b, *mW, *vW, *mb, *vb;
-  float* WT;        // transposed copy to refresh (layer-1 weights) or null
+  float* WT;        // transposed copy [in][ldwt] to refresh
+  int ldwt;         // out rounded up to a multiple of 4 (16-byte rows)
 };
 
 struct MztGradParams {
@@ -61,4 +62,4 @@ struct MztGradParams {
 size_t mzt_rows_smem_bytes(int rows, int U);
 hipError_t mzt_launch_rows(int rows, int support, const MztRowParams& p, hipStream_t stream);
 hipError_t mzt_launch_grad_adam(const MztGradParams& P, int n_tiles, hipStream_t stream);
-hipError_t mzt_launch_transpose(const float* W, float* WT, int out, int in, hipStream_t stream);
+hipError_t mzt_launch_transpose(const float* W, float* WT, int out, int in, int ldwt, hipStream_t stream);

@@ -107,14 +107,80 @@ __device__ __forceinline__ float parab_bwd(const Parab& p, float gout) {
 }
 
 // ------------------------------------------------------------------------------------------
+// k-major GEMV pieces.  Every Linear layer, in both directions, is read from whichever of torch's
+// [out][in] weight or its transposed copy [in][out_pad] has the OUTPUT index contiguous ("k-major":
+// element (k, c) at W[k * ldw + c], rows 16-byte aligned).  Thread t -> (column group cg = t % C4
+// of 4 outputs, input chunk q = t / C4 of Q chunks): one float4 weight load feeds 4 R FMAs, and
+// the Q partial sums of each output are added through LDS by kcomb after a barrier.
+template <int R, int C4, int Q>
+__device__ __forceinline__ void kpart(const float* __restrict__ W, int ldw, int K, const float* X, int ldx,
+                                      float* P) {
+  const int t = threadIdx.x;
+  if (t >= C4 * Q) return;
+  const int cg = t % C4, q = t / C4;
+  const int cs = (K + Q - 1) / Q;
+  const int k0 = q * cs, k1 = min(K, k0 + cs);
+  float4 acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+  for (int k = k0; k < k1; ++k) {
+    const float4 w = *(const float4*)(W + (size_t)k * ldw + 4 * cg);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float x = X[r * ldx + k];
+      acc[r].x = fmaf(w.x, x, acc[r].x);
+      acc[r].y = fmaf(w.y, x, acc[r].y);
+      acc[r].z = fmaf(w.z, x, acc[r].z);
+      acc[r].w = fmaf(w.w, x, acc[r].w);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) *(float4*)(P + (q * R + r) * (4 * C4) + 4 * cg) = acc[r];
+}
+// the same with float2 loads for a weight whose rows are only 8-byte aligned (dynamics layer 1,
+// [256][70]); C2 column pairs
+template <int R, int C2, int Q>
+__device__ __forceinline__ void kpart2(const float* __restrict__ W, int ldw, int K, const float* X, int ldx,
+                                       float* P) {
+  const int t = threadIdx.x;
+  if (t >= C2 * Q) return;
+  const int cg = t % C2, q = t / C2;
+  const int cs = (K + Q - 1) / Q;
+  const int k0 = q * cs, k1 = min(K, k0 + cs);
+  float2 acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = make_float2(0.f, 0.f);
+#pragma unroll 4
+  for (int k = k0; k < k1; ++k) {
+    const float2 w = *(const float2*)(W + (size_t)k * ldw + 2 * cg);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float x = X[r * ldx + k];
+      acc[r].x = fmaf(w.x, x, acc[r].x);
+      acc[r].y = fmaf(w.y, x, acc[r].y);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) *(float2*)(P + (q * R + r) * (2 * C2) + 2 * cg) = acc[r];
+}
+// sum of the Q partials of output c of row r (fixed order q = 0..Q-1)
+template <int R, int Q>
+__device__ __forceinline__ float kcomb(const float* P, int ldp, int r, int c) {
+  float v = 0.f;
+#pragma unroll
+  for (int q = 0; q < Q; ++q) v += P[(q * R + r) * ldp + c];
+  return v;
+}
+
 // LDS plan of the rows kernel (floats), U steps, R rows
+constexpr int RED_PER_ROW = 3072;  // split-K partials: 3 matrices x 4 chunks x 256 outputs
 template <int R>
 struct RowLds {
-  int U;
   // multiple of 4 floats: the per-step activation rows are read as float4
   __device__ __host__ static int per_step() { return (R * (4 * F + H + 8 + 48 + 48) + 2 * R + 3) & ~3; }
   __device__ __host__ static int fixed() {
-    return R * (32 + F + H + H + H + H + 8 + 48 + 48 + 4 * F + NT) + 8 * R + 64;
+    return R * (32 + F + H + H + H + H + 8 + 48 + 48 + 4 * F + RED_PER_ROW) + 8 * R + 64;
   }
   __device__ __host__ static size_t bytes(int U) { return sizeof(float) * (size_t)(fixed() + U * per_step()); }
 };
@@ -127,6 +193,8 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
   const int b0 = blockIdx.x * R;
   constexpr int LDS_SUP = 48;
   constexpr int LD_GS = SUP > 1 ? 48 : 16;  // padded widths of the GY logit arrays (kernel 2 reads 16-col tiles)
+  constexpr int LDV = (SUP + 3) & ~3;       // row stride of the value / reward layer-2 transposed copies
+  constexpr int CV = LDV / 4;
 
   // ---- LDS carve-up
   float* x0 = lds;                    // [R][32]
@@ -142,8 +210,10 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
   float* gvh = gph + R * F;
   float* grh = gvh + R * F;
   float* gdh = grh + R * F;
-  float* red = gdh + R * F;          // [Q][R][NC] split-K partial sums (<= 256 R floats)
-  float* rowf = red + R * NT;         // [8][R] per-row scalars: 0 v_loss, 1 r_loss, 2 p_loss, 3 g_b
+  float* red = gdh + R * F;           // split-K partials, RED_PER_ROW * R floats
+  float* red1 = red + R * 1024;       // second and third partial areas (1024 R floats each)
+  float* red2 = red + R * 2048;
+  float* rowf = red + R * RED_PER_ROW;  // [8][R] per-row scalars: 0 v_loss, 1 r_loss, 2 p_loss, 3 g_b
   int* acts = (int*)(rowf + 8 * R);   // [64] actions (R*U <= 64)
   float* st = (float*)(acts + 64);    // per-step block
   const int PS = RowLds<R>::per_step();
@@ -179,45 +249,20 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
   __syncthreads();
 
   // ---- representation: hidden, output, normalise
-  {
-    float acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = 0.f;
-    for (int k = 0; k < p.in_dim; ++k) {
-      const float wk = n.rep1T[k * F + tid];
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = fmaf(wk, x0[r * 32 + k], acc[r]);
-    }
-    const float bj = n.rep1b[tid];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const float a = fmaxf(acc[r] + bj, 0.f);
-      repa[r * F + tid] = a;
-      if (valid(r)) s.repa[(size_t)(b0 + r) * F + tid] = a;
-    }
+  kpart<R, 64, 4>(n.rep1T, F, p.in_dim, x0, 32, red);
+  __syncthreads();
+  for (int i = tid; i < R * F; i += NT) {
+    const int r = i / F, c = i - r * F;
+    const float a = fmaxf(kcomb<R, 4>(red, F, r, c) + n.rep1b[c], 0.f);
+    repa[i] = a;
+    if (valid(r)) s.repa[(size_t)(b0 + r) * F + c] = a;
   }
   __syncthreads();
-  {
-    using SK = SplitK<H>;
-    const int c = tid % H, q = tid / H;
-    float acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = 0.f;
-#pragma unroll 8
-    for (int k = q * SK::CS; k < (q + 1) * SK::CS; ++k) {
-      const float w = n.rep2T[k * H + c];
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = fmaf(w, repa[r * F + k], acc[r]);
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) red[(q * R + r) * H + c] = acc[r];
-  }
+  kpart<R, 16, 16>(n.rep2T, H, F, repa, F, red);
   __syncthreads();
   for (int i = tid; i < R * H; i += NT) {
     const int r = i / H, c = i - r * H;
-    float v = 0.f;
-    for (int q = 0; q < SplitK<H>::Q; ++q) v += red[(q * R + r) * H + c];
-    hp0[i] = v + n.rep2b[c];
+    hp0[i] = kcomb<R, 16>(red, H, r, c) + n.rep2b[c];
   }
   __syncthreads();
   for (int r = wave; r < R; r += 4) {
@@ -240,81 +285,43 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
     float* lv = s_lv(t);
     float* lr = s_lr(t);
     float* vr = s_vr(t);
-    // S1: policy / value / dynamics hidden layers (all read h_t)
-    {
-      float cp[R], cv[R], cd[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) cp[r] = cv[r] = cd[r] = 0.f;
-#pragma unroll 4
-      for (int k = 0; k < H; ++k) {
-        const float wp = n.pol1T[k * F + tid], wv = n.val1T[k * F + tid], wd = n.dyn1T[k * F + tid];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const float x = h[r * H + k];
-          cp[r] = fmaf(wp, x, cp[r]);
-          cv[r] = fmaf(wv, x, cv[r]);
-          cd[r] = fmaf(wd, x, cd[r]);
-        }
-      }
-      const float bp = n.pol1b[tid], bv = n.val1b[tid], bd = n.dyn1b[tid];
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        cd[r] += n.dyn1T[(H + acts[r * U + t]) * F + tid];  // the one-hot action column
-        const float a1 = fmaxf(cp[r] + bp, 0.f), a2 = fmaxf(cv[r] + bv, 0.f), a3 = fmaxf(cd[r] + bd, 0.f);
-        ap[r * F + tid] = a1;
-        av[r * F + tid] = a2;
-        ad[r * F + tid] = a3;
-        if (valid(r)) {
-          const size_t m = (size_t)(b0 + r) * U + t;
-          s.ap[m * F + tid] = a1;
-          s.av[m * F + tid] = a2;
-          s.ad[m * F + tid] = a3;
-        }
+    // S1: policy / value / dynamics hidden layers, all on h_t (dynamics' one-hot column added below)
+    kpart<R, 64, 4>(n.pol1T, F, H, h, H, red);
+    kpart<R, 64, 4>(n.val1T, F, H, h, H, red1);
+    kpart<R, 64, 4>(n.dyn1T, F, H, h, H, red2);
+    __syncthreads();
+    for (int i = tid; i < R * F; i += NT) {
+      const int r = i / F, c = i - r * F;
+      const float a1 = fmaxf(kcomb<R, 4>(red, F, r, c) + n.pol1b[c], 0.f);
+      const float a2 = fmaxf(kcomb<R, 4>(red1, F, r, c) + n.val1b[c], 0.f);
+      const float a3 = fmaxf((kcomb<R, 4>(red2, F, r, c) + n.dyn1T[(H + acts[r * U + t]) * F + c]) + n.dyn1b[c], 0.f);
+      ap[i] = a1;
+      av[i] = a2;
+      ad[i] = a3;
+      if (valid(r)) {
+        const size_t m = (size_t)(b0 + r) * U + t;
+        s.ap[m * F + c] = a1;
+        s.av[m * F + c] = a2;
+        s.ad[m * F + c] = a3;
       }
     }
     __syncthreads();
-    // S2: policy logits (6), value logits (SUP), dynamics output h'_{t+1} (64): split-K over the
-    //     transposed layer-2 copies, partial sums combined in a second pass
-    {
-      constexpr int NC = A + SUP + H;
-      using SK = SplitK<NC>;
-      if (tid < NC * SK::Q) {
-        const int c = tid % NC, q = tid / NC;
-        const float* WT;
-        const float* act;
-        int nout, o;
-        if (c < A) {
-          WT = n.pol2T; act = ap; nout = A; o = c;
-        } else if (c < A + SUP) {
-          WT = n.val2T; act = av; nout = SUP; o = c - A;
-        } else {
-          WT = n.dyn2T; act = ad; nout = H; o = c - A - SUP;
-        }
-        float acc[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = 0.f;
-        const int k1 = min(F, (q + 1) * SK::CS);
-#pragma unroll 8
-        for (int k = q * SK::CS; k < k1; ++k) {
-          const float w = WT[k * nout + o];
-#pragma unroll
-          for (int r = 0; r < R; ++r) acc[r] = fmaf(w, act[r * F + k], acc[r]);
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) red[(q * R + r) * NC + c] = acc[r];
-      }
-      __syncthreads();
-      for (int i = tid; i < R * NC; i += NT) {
-        const int r = i / NC, c = i - r * NC;
-        float v = 0.f;
-        for (int q = 0; q < SK::Q; ++q) v += red[(q * R + r) * NC + c];
-        if (c < A)
-          lp[r * 8 + c] = v + n.pol2b[c];
-        else if (c < A + SUP)
-          lv[r * LDS_SUP + c - A] = v + n.val2b[c - A];
-        else
-          hp[r * H + c - A - SUP] = v + n.dyn2b[c - A - SUP];
-      }
+    // S2: policy logits, value logits, dynamics output h'_{t+1}: split-K over the transposed copies
+    kpart<R, 2, 32>(n.pol2T, 8, F, ap, F, red);
+    kpart<R, CV, NT / CV < 64 ? NT / CV : 64>(n.val2T, LDV, F, av, F, red1);
+    kpart<R, 16, 16>(n.dyn2T, H, F, ad, F, red2);
+    __syncthreads();
+    for (int i = tid; i < R * H; i += NT) {
+      const int r = i / H, c = i - r * H;
+      hp[i] = kcomb<R, 16>(red2, H, r, c) + n.dyn2b[c];
+    }
+    for (int i = tid; i < R * SUP; i += NT) {
+      const int r = i / SUP, c = i - r * SUP;
+      lv[r * LDS_SUP + c] = kcomb<R, (NT / CV < 64 ? NT / CV : 64)>(red1, LDV, r, c) + n.val2b[c];
+    }
+    for (int i = tid; i < R * A; i += NT) {
+      const int r = i / A, c = i - r * A;
+      lp[r * 8 + c] = kcomb<R, 32>(red, 8, r, c) + n.pol2b[c];
     }
     __syncthreads();
     // S3: normalise h'_{t+1} -> h_{t+1} (one wave per row), reward hidden layer on h'_{t+1}
@@ -329,50 +336,21 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
         if (t + 1 < U) s.h[(m + 1) * H + lane] = y;
       }
     }
-    {
-      float c[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) c[r] = 0.f;
-#pragma unroll 4
-      for (int k = 0; k < H; ++k) {
-        const float wk = n.rwd1T[k * F + tid];
-#pragma unroll
-        for (int r = 0; r < R; ++r) c[r] = fmaf(wk, hp[r * H + k], c[r]);
-      }
-      const float bj = n.rwd1b[tid];
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const float a = fmaxf(c[r] + bj, 0.f);
-        ar[r * F + tid] = a;
-        if (valid(r)) s.ar[((size_t)(b0 + r) * U + t) * F + tid] = a;
-      }
+    kpart<R, 64, 4>(n.rwd1T, F, H, hp, H, red);
+    __syncthreads();
+    for (int i = tid; i < R * F; i += NT) {
+      const int r = i / F, c = i - r * F;
+      const float a = fmaxf(kcomb<R, 4>(red, F, r, c) + n.rwd1b[c], 0.f);
+      ar[i] = a;
+      if (valid(r)) s.ar[((size_t)(b0 + r) * U + t) * F + c] = a;
     }
     __syncthreads();
-    // S4: reward logits (split-K)
-    {
-      using SK = SplitK<SUP>;
-      if (tid < SUP * SK::Q) {
-        const int c = tid % SUP, q = tid / SUP;
-        float acc[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = 0.f;
-        const int k1 = min(F, (q + 1) * SK::CS);
-#pragma unroll 8
-        for (int k = q * SK::CS; k < k1; ++k) {
-          const float w = n.rwd2T[k * SUP + c];
-#pragma unroll
-          for (int r = 0; r < R; ++r) acc[r] = fmaf(w, ar[r * F + k], acc[r]);
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) red[(q * R + r) * SUP + c] = acc[r];
-      }
-      __syncthreads();
-      for (int i = tid; i < R * SUP; i += NT) {
-        const int r = i / SUP, c = i - r * SUP;
-        float v = 0.f;
-        for (int q = 0; q < SK::Q; ++q) v += red[(q * R + r) * SUP + c];
-        lr[r * LDS_SUP + c] = v + n.rwd2b[c];
-      }
+    // S4: reward logits
+    kpart<R, CV, NT / CV < 64 ? NT / CV : 64>(n.rwd2T, LDV, F, ar, F, red);
+    __syncthreads();
+    for (int i = tid; i < R * SUP; i += NT) {
+      const int r = i / SUP, c = i - r * SUP;
+      lr[r * LDS_SUP + c] = kcomb<R, (NT / CV < 64 ? NT / CV : 64)>(red, LDV, r, c) + n.rwd2b[c];
     }
     __syncthreads();
     // S5: heads and loss terms; task = (head, row), heads: 0 value, 1 reward, 2 policy
@@ -485,111 +463,56 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
       }
     }
     __syncthreads();
-    // B2: hidden-layer gradients of the reward, value and policy heads (thread = hidden unit)
-    {
-      float cr[R], cv[R], cp[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) cr[r] = cv[r] = cp[r] = 0.f;
-      for (int o = 0; o < SUP; ++o) {
-        const float wr = n.rwd2[o * F + tid], wv = n.val2[o * F + tid];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          cr[r] = fmaf(wr, glr[r * 48 + o], cr[r]);
-          cv[r] = fmaf(wv, glv[r * 48 + o], cv[r]);
-        }
-      }
-#pragma unroll
-      for (int o = 0; o < A; ++o) {
-        const float wp = n.pol2[o * F + tid];
-#pragma unroll
-        for (int r = 0; r < R; ++r) cp[r] = fmaf(wp, glp[r * 8 + o], cp[r]);
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const float g1 = ar[r * F + tid] > 0.f ? cr[r] : 0.f;
-        const float g2 = av[r * F + tid] > 0.f ? cv[r] : 0.f;
-        const float g3 = ap[r * F + tid] > 0.f ? cp[r] : 0.f;
-        grh[r * F + tid] = g1;
-        gvh[r * F + tid] = g2;
-        gph[r * F + tid] = g3;
-        if (valid(r)) {
-          const size_t m = (size_t)(b0 + r) * U + t;
-          s.g_r[m * F + tid] = g1;
-          s.g_v[m * F + tid] = g2;
-          s.g_p[m * F + tid] = g3;
-        }
+    // B2: hidden-layer gradients of the reward, value and policy heads through torch's [out][256]
+    //     layer-2 weights (k-major over the logits)
+    kpart<R, 64, 4>(n.rwd2, F, SUP, glr, 48, red);
+    kpart<R, 64, 4>(n.val2, F, SUP, glv, 48, red1);
+    kpart<R, 64, 4>(n.pol2, F, A, glp, 8, red2);
+    __syncthreads();
+    for (int i = tid; i < R * F; i += NT) {
+      const int r = i / F, c = i - r * F;
+      const float g1 = ar[i] > 0.f ? kcomb<R, 4>(red, F, r, c) : 0.f;
+      const float g2 = av[i] > 0.f ? kcomb<R, 4>(red1, F, r, c) : 0.f;
+      const float g3 = ap[i] > 0.f ? kcomb<R, 4>(red2, F, r, c) : 0.f;
+      grh[i] = g1;
+      gvh[i] = g2;
+      gph[i] = g3;
+      if (valid(r)) {
+        const size_t m = (size_t)(b0 + r) * U + t;
+        s.g_r[m * F + c] = g1;
+        s.g_v[m * F + c] = g2;
+        s.g_p[m * F + c] = g3;
       }
     }
     __syncthreads();
-    // B3: h'_{t+1} gradient += reward layer-1 backward (split-K over the 256 hidden units,
-    //     torch's own [256][64] layout: coalesced over the 64 outputs)
-    {
-      const int k = tid & 63, q = tid >> 6;
-      float acc[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = 0.f;
-#pragma unroll 8
-      for (int j = 64 * q; j < 64 * q + 64; ++j) {
-        const float w = n.rwd1[j * H + k];
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = fmaf(w, grh[r * F + j], acc[r]);
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) red[(q * R + r) * H + k] = acc[r];
-    }
+    // B3: h'_{t+1} gradient += reward layer-1 backward (torch's [256][64]: k-major over the hidden units)
+    kpart<R, 16, 16>(n.rwd1, H, F, grh, F, red);
     __syncthreads();
     for (int i = tid; i < R * H; i += NT) {
-      const int r = i / H, k = i - r * H;
-      const float v = ghp[i] + (((red[(0 * R + r) * H + k] + red[(1 * R + r) * H + k]) + red[(2 * R + r) * H + k]) +
-                                red[(3 * R + r) * H + k]);
+      const int r = i / H, c = i - r * H;
+      const float v = ghp[i] + kcomb<R, 16>(red, H, r, c);
       ghp[i] = v;
-      if (valid(r)) s.g_hp[((size_t)(b0 + r) * U + t) * H + k] = v;
+      if (valid(r)) s.g_hp[((size_t)(b0 + r) * U + t) * H + c] = v;
     }
     __syncthreads();
-    // B4: dynamics hidden gradient
-    {
-      float c[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) c[r] = 0.f;
-#pragma unroll 4
-      for (int o = 0; o < H; ++o) {
-        const float w = n.dyn2[o * F + tid];
-#pragma unroll
-        for (int r = 0; r < R; ++r) c[r] = fmaf(w, ghp[r * H + o], c[r]);
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const float g = ad[r * F + tid] > 0.f ? c[r] : 0.f;
-        gdh[r * F + tid] = g;
-        if (valid(r)) s.g_d[((size_t)(b0 + r) * U + t) * F + tid] = g;
-      }
+    // B4: dynamics hidden gradient (torch's [64][256] layer-2 weight)
+    kpart<R, 64, 4>(n.dyn2, F, H, ghp, H, red);
+    __syncthreads();
+    for (int i = tid; i < R * F; i += NT) {
+      const int r = i / F, c = i - r * F;
+      const float g = ad[i] > 0.f ? kcomb<R, 4>(red, F, r, c) : 0.f;
+      gdh[i] = g;
+      if (valid(r)) s.g_d[((size_t)(b0 + r) * U + t) * F + c] = g;
     }
     __syncthreads();
-    // B5: gradient of h_t = dynamics + value + policy layer-1 backward (latent columns only),
-    //     split-K over the hidden units in torch's layouts ([256][70], [256][64], [256][64])
-    {
-      const int k = tid & 63, q = tid >> 6;
-      float acc[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = 0.f;
-#pragma unroll 4
-      for (int j = 64 * q; j < 64 * q + 64; ++j) {
-        const float wd = n.dyn1[j * (H + A) + k], wv = n.val1[j * H + k], wp = n.pol1[j * H + k];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          acc[r] = fmaf(wd, gdh[r * F + j], acc[r]);
-          acc[r] = fmaf(wv, gvh[r * F + j], acc[r]);
-          acc[r] = fmaf(wp, gph[r * F + j], acc[r]);
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) red[(q * R + r) * H + k] = acc[r];
-    }
+    // B5: gradient of h_t = dynamics + value + policy layer-1 backward (latent columns only)
+    kpart2<R, 32, 8>(n.dyn1, H + A, F, gdh, F, red);
+    kpart<R, 16, 16>(n.val1, H, F, gvh, F, red1);
+    kpart<R, 16, 16>(n.pol1, H, F, gph, F, red2);
     __syncthreads();
     for (int i = tid; i < R * H; i += NT) {
-      const int r = i / H, k = i - r * H;
-      gh[i] = ((red[(0 * R + r) * H + k] + red[(1 * R + r) * H + k]) + red[(2 * R + r) * H + k]) +
-              red[(3 * R + r) * H + k];
+      const int r = i / H, c = i - r * H;
+      gh[i] = (kcomb<R, 8>(red, H, r, c) + kcomb<R, 16>(red1, H, r, c)) + kcomb<R, 16>(red2, H, r, c);
     }
     __syncthreads();
   }
@@ -612,21 +535,12 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
     if (valid(r)) s.g_h0p[(size_t)(b0 + r) * H + lane] = gv;
   }
   __syncthreads();
-  {
-    float c[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) c[r] = 0.f;
-#pragma unroll 4
-    for (int o = 0; o < H; ++o) {
-      const float w = n.rep2[o * F + tid];
-#pragma unroll
-      for (int r = 0; r < R; ++r) c[r] = fmaf(w, ghp[r * H + o], c[r]);
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const float g = repa[r * F + tid] > 0.f ? c[r] : 0.f;
-      if (valid(r)) s.g_rep[(size_t)(b0 + r) * F + tid] = g;
-    }
+  kpart<R, 64, 4>(n.rep2, F, H, ghp, H, red);
+  __syncthreads();
+  for (int i = tid; i < R * F; i += NT) {
+    const int r = i / F, c = i - r * F;
+    const float g = repa[i] > 0.f ? kcomb<R, 4>(red, F, r, c) : 0.f;
+    if (valid(r)) s.g_rep[(size_t)(b0 + r) * F + c] = g;
   }
   if (tid < R && valid(tid)) {
     const int r = tid;
@@ -650,9 +564,14 @@ __device__ __forceinline__ void adam(float* pp, float* mm, float* vv, size_t i, 
   vv[i] = v;
 }
 
-__global__ __launch_bounds__(NT, 2) void mzt_grad_adam_kernel(MztGradParams P) {
-  __shared__ float red[4][16][17];
-  __shared__ float bred[16][17];
+#ifndef MZT_NW2
+#define MZT_NW2 8
+#endif
+constexpr int NW2 = MZT_NW2;  // waves per weight tile: they split the B*U rows
+__global__ __launch_bounds__(64 * NW2) void mzt_grad_adam_kernel(MztGradParams P) {
+  constexpr int NP = 4 * NW2;  // bias row classes (16 columns x NP)
+  __shared__ float red[NW2][16][17];
+  __shared__ float bred[NP][17];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int li = 0;
   while (li < 9 && (int)blockIdx.x >= P.L[li + 1].tile0) ++li;
@@ -669,13 +588,13 @@ __global__ __launch_bounds__(NT, 2) void mzt_grad_adam_kernel(MztGradParams P) {
   const bool onehot = L.onehot_from >= 0 && k0 >= L.onehot_from;
   const int act_col = kc - L.onehot_from;
   const bool kin = kc < L.in;
-  // rows m = 16 i + 4 wave + sub; loads batched ahead of the MFMA chain
-  constexpr int UNR = 8;
-  for (int base = 4 * wave; base < L.M; base += 16 * UNR) {
+  // rows m = 4 (wave + NW2 i) + sub; loads batched ahead of the MFMA chain
+  constexpr int UNR = 8, STEP = 4 * NW2;
+  for (int base = 4 * wave; base < L.M; base += STEP * UNR) {
     float a[UNR], b[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const int m = base + 16 * u + sub;
+      const int m = base + STEP * u + sub;
       const bool ok = m < L.M;
       a[u] = ok ? L.GY[(size_t)m * L.ldg + oc] : 0.f;
       if (onehot)
@@ -689,15 +608,15 @@ __global__ __launch_bounds__(NT, 2) void mzt_grad_adam_kernel(MztGradParams P) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[wave][4 * sub + r][col] = acc[r];
   if (kb == 0) {
-    // bias: sum of GY column o0 + (tid & 15) over rows m = tid >> 4 (mod 16), 8 independent sums
+    // bias: sum of GY column o0 + (tid & 15) over rows m = tid >> 4 (mod NP), UNR independent sums
     const int i = tid & 15, part = tid >> 4;
     float sb[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) sb[u] = 0.f;
-    for (int m = part; m < L.M; m += 16 * UNR) {
+    for (int m = part; m < L.M; m += NP * UNR) {
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        const int mm = m + 16 * u;
+        const int mm = m + NP * u;
         sb[u] += mm < L.M ? L.GY[(size_t)mm * L.ldg + o0 + i] : 0.f;
       }
     }
@@ -707,28 +626,30 @@ __global__ __launch_bounds__(NT, 2) void mzt_grad_adam_kernel(MztGradParams P) {
     bred[part][i] = t;
   }
   __syncthreads();
-  {
+  if (tid < 256) {
     const int i = tid >> 4, j = tid & 15;
     const int o = o0 + i, k = k0 + j;
     if (o < L.out && k < L.in) {
-      const float g = ((red[0][i][j] + red[1][i][j]) + red[2][i][j]) + red[3][i][j];
+      float g = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW2; ++w) g += red[w][i][j];
       const size_t idx = (size_t)o * L.in + k;
       adam(L.W, L.mW, L.vW, idx, g, P);
-      L.WT[(size_t)k * L.out + o] = L.W[idx];
+      L.WT[(size_t)k * L.ldwt + o] = L.W[idx];
     }
   }
   if (kb == 0 && tid < 16 && o0 + tid < L.out) {
     float g = 0.f;
-    for (int part = 0; part < 16; ++part) g += bred[part][tid];
+    for (int part = 0; part < NP; ++part) g += bred[part][tid];
     adam(L.b, L.mb, L.vb, o0 + tid, g, P);
   }
 }
 
-__global__ void mzt_transpose_kernel(const float* W, float* WT, int out, int in) {
+__global__ void mzt_transpose_kernel(const float* W, float* WT, int out, int in, int ldwt) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < out * in) {
-    const int o = i / in, k = i - o * in;
-    WT[(size_t)k * out + o] = W[i];
+  if (i < ldwt * in) {
+    const int k = i / ldwt, o = i - k * ldwt;
+    WT[i] = o < out ? W[(size_t)o * in + k] : 0.f;  // pad columns stay zero
   }
 }
 
@@ -744,32 +665,20 @@ hipError_t launch_rows(const MztRowParams& p, hipStream_t stream) {
 
 }  // namespace
 
-size_t mzt_rows_smem_bytes(int rows, int U) {
-  switch (rows) {
-    case 1: return RowLds<1>::bytes(U);
-    case 2: return RowLds<2>::bytes(U);
-    default: return RowLds<4>::bytes(U);
-  }
-}
+size_t mzt_rows_smem_bytes(int rows, int U) { return rows == 1 ? RowLds<1>::bytes(U) : RowLds<2>::bytes(U); }
 
 hipError_t mzt_launch_rows(int rows, int support, const MztRowParams& p, hipStream_t stream) {
-  if (support == 33) {
-    if (rows == 1) return launch_rows<1, 33>(p, stream);
-    if (rows == 2) return launch_rows<2, 33>(p, stream);
-    return launch_rows<4, 33>(p, stream);
-  }
-  if (rows == 1) return launch_rows<1, 1>(p, stream);
-  if (rows == 2) return launch_rows<2, 1>(p, stream);
-  return launch_rows<4, 1>(p, stream);
+  if (support == 33) return rows == 1 ? launch_rows<1, 33>(p, stream) : launch_rows<2, 33>(p, stream);
+  return rows == 1 ? launch_rows<1, 1>(p, stream) : launch_rows<2, 1>(p, stream);
 }
 
 hipError_t mzt_launch_grad_adam(const MztGradParams& P, int n_tiles, hipStream_t stream) {
-  hipLaunchKernelGGL(mzt_grad_adam_kernel, dim3(n_tiles), dim3(NT), 0, stream, P);
+  hipLaunchKernelGGL(mzt_grad_adam_kernel, dim3(n_tiles), dim3(64 * NW2), 0, stream, P);
   return hipGetLastError();
 }
 
-hipError_t mzt_launch_transpose(const float* W, float* WT, int out, int in, hipStream_t stream) {
-  const int n = out * in;
-  hipLaunchKernelGGL(mzt_transpose_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, W, WT, out, in);
+hipError_t mzt_launch_transpose(const float* W, float* WT, int out, int in, int ldwt, hipStream_t stream) {
+  const int n = ldwt * in;
+  hipLaunchKernelGGL(mzt_transpose_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, W, WT, out, in, ldwt);
   return hipGetLastError();
 }

@@ -281,7 +281,9 @@ class FusedUpdate:
         self.support = net.support_size
         self.in_dim = self.params[0].shape[1]
         dev = self.params[0].device
-        self.wt = [torch.empty(p.shape[1], p.shape[0], dtype=torch.float32, device=dev) for p in self.params[0::2]]
+        # transposed weight copies [in][out rounded up to 4] (16-byte rows for float4 loads)
+        self.wt = [torch.zeros(p.shape[1], (p.shape[0] + 3) // 4 * 4, dtype=torch.float32, device=dev)
+                   for p in self.params[0::2]]
         self.scratch = None
         self.B = None
         self._seen = None  # parameter versions after our own last write
