@@ -63,12 +63,6 @@ __device__ __forceinline__ float wave_min(float v) {
   return wave_reduce(v, [](float a, float b) { return fminf(a, b); });
 }
 
-// split-K GEMV pieces: thread -> (output c < NC, chunk q < Q of the K = 256 inputs)
-template <int NC>
-struct SplitK {
-  static constexpr int Q = (NT / NC) < 16 ? (NT / NC) : 16;
-  static constexpr int CS = (F + Q - 1) / Q;
-};
 // first lane index holding `v` among lanes where `hit` (ties -> lowest index, torch-CPU's choice)
 __device__ __forceinline__ int wave_first(bool hit) {
   const unsigned long long m = __ballot(hit);
@@ -173,8 +167,14 @@ __device__ __forceinline__ float kcomb(const float* P, int ldp, int r, int c) {
   return v;
 }
 
+// threads of a row-kernel workgroup (256: one wave per SIMD; 512: two)
+#ifndef MZT_RNT
+#define MZT_RNT 512
+#endif
+constexpr int RNT = MZT_RNT;
+
 // LDS plan of the rows kernel (floats), U steps, R rows
-constexpr int RED_PER_ROW = 3072;  // split-K partials: 3 matrices x 4 chunks x 256 outputs
+constexpr int RED_PER_ROW = 12 * RNT;  // split-K partials: 3 areas x (RNT / 64 chunks x 256 outputs)
 template <int R>
 struct RowLds {
   // multiple of 4 floats: the per-step activation rows are read as float4
@@ -186,7 +186,7 @@ struct RowLds {
 };
 
 template <int R, int SUP>
-__global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
+__global__ __launch_bounds__(RNT, 1) void mzt_rows_kernel(MztRowParams p) {
   extern __shared__ float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int U = p.U, B = p.B;
@@ -211,8 +211,8 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
   float* grh = gvh + R * F;
   float* gdh = grh + R * F;
   float* red = gdh + R * F;           // split-K partials, RED_PER_ROW * R floats
-  float* red1 = red + R * 1024;       // second and third partial areas (1024 R floats each)
-  float* red2 = red + R * 2048;
+  float* red1 = red + R * 4 * RNT;    // second and third partial areas (4 RNT R floats each)
+  float* red2 = red + R * 8 * RNT;
   float* rowf = red + R * RED_PER_ROW;  // [8][R] per-row scalars: 0 v_loss, 1 r_loss, 2 p_loss, 3 g_b
   int* acts = (int*)(rowf + 8 * R);   // [64] actions (R*U <= 64)
   float* st = (float*)(acts + 64);    // per-step block
@@ -233,13 +233,13 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
   auto valid = [&](int r) { return b0 + r < B; };
 
   // ---- inputs
-  for (int i = tid; i < R * 32; i += NT) {
+  for (int i = tid; i < R * 32; i += RNT) {
     const int r = i >> 5, k = i & 31;
     const float v = k < p.in_dim ? p.obs[(size_t)rowb(r) * p.in_dim + k] : 0.f;
     x0[i] = v;
     if (valid(r)) s.x0[(size_t)(b0 + r) * 32 + k] = v;
   }
-  for (int i = tid; i < R * U; i += NT) acts[i] = (int)p.actions[(size_t)rowb(i / U) * U + (i % U)];
+  for (int i = tid; i < R * U; i += RNT) acts[i] = (int)p.actions[(size_t)rowb(i / U) * U + (i % U)];
   if (tid < R) {
     const int r = tid;
     rowf[0 * R + r] = rowf[1 * R + r] = rowf[2 * R + r] = 0.f;
@@ -249,23 +249,23 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
   __syncthreads();
 
   // ---- representation: hidden, output, normalise
-  kpart<R, 64, 4>(n.rep1T, F, p.in_dim, x0, 32, red);
+  kpart<R, 64, RNT / 64>(n.rep1T, F, p.in_dim, x0, 32, red);
   __syncthreads();
-  for (int i = tid; i < R * F; i += NT) {
+  for (int i = tid; i < R * F; i += RNT) {
     const int r = i / F, c = i - r * F;
-    const float a = fmaxf(kcomb<R, 4>(red, F, r, c) + n.rep1b[c], 0.f);
+    const float a = fmaxf(kcomb<R, RNT / 64>(red, F, r, c) + n.rep1b[c], 0.f);
     repa[i] = a;
     if (valid(r)) s.repa[(size_t)(b0 + r) * F + c] = a;
   }
   __syncthreads();
-  kpart<R, 16, 16>(n.rep2T, H, F, repa, F, red);
+  kpart<R, 16, RNT / 16>(n.rep2T, H, F, repa, F, red);
   __syncthreads();
-  for (int i = tid; i < R * H; i += NT) {
+  for (int i = tid; i < R * H; i += RNT) {
     const int r = i / H, c = i - r * H;
-    hp0[i] = kcomb<R, 16>(red, H, r, c) + n.rep2b[c];
+    hp0[i] = kcomb<R, RNT / 16>(red, H, r, c) + n.rep2b[c];
   }
   __syncthreads();
-  for (int r = wave; r < R; r += 4) {
+  for (int r = wave; r < R; r += RNT / 64) {
     const float v = hp0[r * H + lane];
     const float mn = wave_min(v), mx = wave_max(v);
     const float y = (v - mn) / ((mx - mn) + 1e-8f);
@@ -286,15 +286,15 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
     float* lr = s_lr(t);
     float* vr = s_vr(t);
     // S1: policy / value / dynamics hidden layers, all on h_t (dynamics' one-hot column added below)
-    kpart<R, 64, 4>(n.pol1T, F, H, h, H, red);
-    kpart<R, 64, 4>(n.val1T, F, H, h, H, red1);
-    kpart<R, 64, 4>(n.dyn1T, F, H, h, H, red2);
+    kpart<R, 64, RNT / 64>(n.pol1T, F, H, h, H, red);
+    kpart<R, 64, RNT / 64>(n.val1T, F, H, h, H, red1);
+    kpart<R, 64, RNT / 64>(n.dyn1T, F, H, h, H, red2);
     __syncthreads();
-    for (int i = tid; i < R * F; i += NT) {
+    for (int i = tid; i < R * F; i += RNT) {
       const int r = i / F, c = i - r * F;
-      const float a1 = fmaxf(kcomb<R, 4>(red, F, r, c) + n.pol1b[c], 0.f);
-      const float a2 = fmaxf(kcomb<R, 4>(red1, F, r, c) + n.val1b[c], 0.f);
-      const float a3 = fmaxf((kcomb<R, 4>(red2, F, r, c) + n.dyn1T[(H + acts[r * U + t]) * F + c]) + n.dyn1b[c], 0.f);
+      const float a1 = fmaxf(kcomb<R, RNT / 64>(red, F, r, c) + n.pol1b[c], 0.f);
+      const float a2 = fmaxf(kcomb<R, RNT / 64>(red1, F, r, c) + n.val1b[c], 0.f);
+      const float a3 = fmaxf((kcomb<R, RNT / 64>(red2, F, r, c) + n.dyn1T[(H + acts[r * U + t]) * F + c]) + n.dyn1b[c], 0.f);
       ap[i] = a1;
       av[i] = a2;
       ad[i] = a3;
@@ -307,25 +307,25 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
     }
     __syncthreads();
     // S2: policy logits, value logits, dynamics output h'_{t+1}: split-K over the transposed copies
-    kpart<R, 2, 32>(n.pol2T, 8, F, ap, F, red);
-    kpart<R, CV, NT / CV < 64 ? NT / CV : 64>(n.val2T, LDV, F, av, F, red1);
-    kpart<R, 16, 16>(n.dyn2T, H, F, ad, F, red2);
+    kpart<R, 2, RNT / 8>(n.pol2T, 8, F, ap, F, red);
+    kpart<R, CV, RNT / CV < 64 ? RNT / CV : 64>(n.val2T, LDV, F, av, F, red1);
+    kpart<R, 16, RNT / 16>(n.dyn2T, H, F, ad, F, red2);
     __syncthreads();
-    for (int i = tid; i < R * H; i += NT) {
+    for (int i = tid; i < R * H; i += RNT) {
       const int r = i / H, c = i - r * H;
-      hp[i] = kcomb<R, 16>(red2, H, r, c) + n.dyn2b[c];
+      hp[i] = kcomb<R, RNT / 16>(red2, H, r, c) + n.dyn2b[c];
     }
-    for (int i = tid; i < R * SUP; i += NT) {
+    for (int i = tid; i < R * SUP; i += RNT) {
       const int r = i / SUP, c = i - r * SUP;
-      lv[r * LDS_SUP + c] = kcomb<R, (NT / CV < 64 ? NT / CV : 64)>(red1, LDV, r, c) + n.val2b[c];
+      lv[r * LDS_SUP + c] = kcomb<R, (RNT / CV < 64 ? RNT / CV : 64)>(red1, LDV, r, c) + n.val2b[c];
     }
-    for (int i = tid; i < R * A; i += NT) {
+    for (int i = tid; i < R * A; i += RNT) {
       const int r = i / A, c = i - r * A;
-      lp[r * 8 + c] = kcomb<R, 32>(red, 8, r, c) + n.pol2b[c];
+      lp[r * 8 + c] = kcomb<R, RNT / 8>(red, 8, r, c) + n.pol2b[c];
     }
     __syncthreads();
     // S3: normalise h'_{t+1} -> h_{t+1} (one wave per row), reward hidden layer on h'_{t+1}
-    for (int r = wave; r < R; r += 4) {
+    for (int r = wave; r < R; r += RNT / 64) {
       const float v = hp[r * H + lane];
       const float mn = wave_min(v), mx = wave_max(v);
       const float y = (v - mn) / ((mx - mn) + 1e-8f);
@@ -336,25 +336,25 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
         if (t + 1 < U) s.h[(m + 1) * H + lane] = y;
       }
     }
-    kpart<R, 64, 4>(n.rwd1T, F, H, hp, H, red);
+    kpart<R, 64, RNT / 64>(n.rwd1T, F, H, hp, H, red);
     __syncthreads();
-    for (int i = tid; i < R * F; i += NT) {
+    for (int i = tid; i < R * F; i += RNT) {
       const int r = i / F, c = i - r * F;
-      const float a = fmaxf(kcomb<R, 4>(red, F, r, c) + n.rwd1b[c], 0.f);
+      const float a = fmaxf(kcomb<R, RNT / 64>(red, F, r, c) + n.rwd1b[c], 0.f);
       ar[i] = a;
       if (valid(r)) s.ar[((size_t)(b0 + r) * U + t) * F + c] = a;
     }
     __syncthreads();
     // S4: reward logits
-    kpart<R, CV, NT / CV < 64 ? NT / CV : 64>(n.rwd2T, LDV, F, ar, F, red);
+    kpart<R, CV, RNT / CV < 64 ? RNT / CV : 64>(n.rwd2T, LDV, F, ar, F, red);
     __syncthreads();
-    for (int i = tid; i < R * SUP; i += NT) {
+    for (int i = tid; i < R * SUP; i += RNT) {
       const int r = i / SUP, c = i - r * SUP;
-      lr[r * LDS_SUP + c] = kcomb<R, (NT / CV < 64 ? NT / CV : 64)>(red, LDV, r, c) + n.rwd2b[c];
+      lr[r * LDS_SUP + c] = kcomb<R, (RNT / CV < 64 ? RNT / CV : 64)>(red, LDV, r, c) + n.rwd2b[c];
     }
     __syncthreads();
     // S5: heads and loss terms; task = (head, row), heads: 0 value, 1 reward, 2 policy
-    for (int task = wave; task < 3 * R; task += 4) {
+    for (int task = wave; task < 3 * R; task += RNT / 64) {
       const int hd = task / R, r = task - hd * R;
       const int bb = rowb(r);
       if (hd < 2) {
@@ -392,7 +392,7 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
   }
 
   // ---- backward through the unroll
-  for (int i = tid; i < R * H; i += NT) gh[i] = 0.f;
+  for (int i = tid; i < R * H; i += RNT) gh[i] = 0.f;
   __syncthreads();
   for (int t = U - 1; t >= 0; --t) {
     const float* ap = s_ap(t);
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
     const float* vr = s_vr(t);
     // B1: head gradients (tasks 0..3R-1) and the normalisation backward of h_{t+1} with the
     //     0.5 hook (tasks 3R..4R-1)
-    for (int task = wave; task < 4 * R; task += 4) {
+    for (int task = wave; task < 4 * R; task += RNT / 64) {
       const int hd = task / R, r = task - hd * R;
       const int bb = rowb(r);
       const size_t m = (size_t)(b0 + r) * U + t;
@@ -465,15 +465,15 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
     __syncthreads();
     // B2: hidden-layer gradients of the reward, value and policy heads through torch's [out][256]
     //     layer-2 weights (k-major over the logits)
-    kpart<R, 64, 4>(n.rwd2, F, SUP, glr, 48, red);
-    kpart<R, 64, 4>(n.val2, F, SUP, glv, 48, red1);
-    kpart<R, 64, 4>(n.pol2, F, A, glp, 8, red2);
+    kpart<R, 64, RNT / 64>(n.rwd2, F, SUP, glr, 48, red);
+    kpart<R, 64, RNT / 64>(n.val2, F, SUP, glv, 48, red1);
+    kpart<R, 64, RNT / 64>(n.pol2, F, A, glp, 8, red2);
     __syncthreads();
-    for (int i = tid; i < R * F; i += NT) {
+    for (int i = tid; i < R * F; i += RNT) {
       const int r = i / F, c = i - r * F;
-      const float g1 = ar[i] > 0.f ? kcomb<R, 4>(red, F, r, c) : 0.f;
-      const float g2 = av[i] > 0.f ? kcomb<R, 4>(red1, F, r, c) : 0.f;
-      const float g3 = ap[i] > 0.f ? kcomb<R, 4>(red2, F, r, c) : 0.f;
+      const float g1 = ar[i] > 0.f ? kcomb<R, RNT / 64>(red, F, r, c) : 0.f;
+      const float g2 = av[i] > 0.f ? kcomb<R, RNT / 64>(red1, F, r, c) : 0.f;
+      const float g3 = ap[i] > 0.f ? kcomb<R, RNT / 64>(red2, F, r, c) : 0.f;
       grh[i] = g1;
       gvh[i] = g2;
       gph[i] = g3;
@@ -486,39 +486,39 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
     }
     __syncthreads();
     // B3: h'_{t+1} gradient += reward layer-1 backward (torch's [256][64]: k-major over the hidden units)
-    kpart<R, 16, 16>(n.rwd1, H, F, grh, F, red);
+    kpart<R, 16, RNT / 16>(n.rwd1, H, F, grh, F, red);
     __syncthreads();
-    for (int i = tid; i < R * H; i += NT) {
+    for (int i = tid; i < R * H; i += RNT) {
       const int r = i / H, c = i - r * H;
-      const float v = ghp[i] + kcomb<R, 16>(red, H, r, c);
+      const float v = ghp[i] + kcomb<R, RNT / 16>(red, H, r, c);
       ghp[i] = v;
       if (valid(r)) s.g_hp[((size_t)(b0 + r) * U + t) * H + c] = v;
     }
     __syncthreads();
     // B4: dynamics hidden gradient (torch's [64][256] layer-2 weight)
-    kpart<R, 64, 4>(n.dyn2, F, H, ghp, H, red);
+    kpart<R, 64, RNT / 64>(n.dyn2, F, H, ghp, H, red);
     __syncthreads();
-    for (int i = tid; i < R * F; i += NT) {
+    for (int i = tid; i < R * F; i += RNT) {
       const int r = i / F, c = i - r * F;
-      const float g = ad[i] > 0.f ? kcomb<R, 4>(red, F, r, c) : 0.f;
+      const float g = ad[i] > 0.f ? kcomb<R, RNT / 64>(red, F, r, c) : 0.f;
       gdh[i] = g;
       if (valid(r)) s.g_d[((size_t)(b0 + r) * U + t) * F + c] = g;
     }
     __syncthreads();
     // B5: gradient of h_t = dynamics + value + policy layer-1 backward (latent columns only)
-    kpart2<R, 32, 8>(n.dyn1, H + A, F, gdh, F, red);
-    kpart<R, 16, 16>(n.val1, H, F, gvh, F, red1);
-    kpart<R, 16, 16>(n.pol1, H, F, gph, F, red2);
+    kpart2<R, 32, RNT / 32>(n.dyn1, H + A, F, gdh, F, red);
+    kpart<R, 16, RNT / 16>(n.val1, H, F, gvh, F, red1);
+    kpart<R, 16, RNT / 16>(n.pol1, H, F, gph, F, red2);
     __syncthreads();
-    for (int i = tid; i < R * H; i += NT) {
+    for (int i = tid; i < R * H; i += RNT) {
       const int r = i / H, c = i - r * H;
-      gh[i] = (kcomb<R, 8>(red, H, r, c) + kcomb<R, 16>(red1, H, r, c)) + kcomb<R, 16>(red2, H, r, c);
+      gh[i] = (kcomb<R, RNT / 32>(red, H, r, c) + kcomb<R, RNT / 16>(red1, H, r, c)) + kcomb<R, RNT / 16>(red2, H, r, c);
     }
     __syncthreads();
   }
 
   // ---- representation backward: normalisation of h_0 (no hook), then the output layer
-  for (int r = wave; r < R; r += 4) {
+  for (int r = wave; r < R; r += RNT / 64) {
     const float v = hp0[r * H + lane];
     const float gy = gh[r * H + lane];
     const float mn = wave_min(v), mxv = wave_max(v);
@@ -535,11 +535,11 @@ __global__ __launch_bounds__(NT, 1) void mzt_rows_kernel(MztRowParams p) {
     if (valid(r)) s.g_h0p[(size_t)(b0 + r) * H + lane] = gv;
   }
   __syncthreads();
-  kpart<R, 64, 4>(n.rep2, F, H, ghp, H, red);
+  kpart<R, 64, RNT / 64>(n.rep2, F, H, ghp, H, red);
   __syncthreads();
-  for (int i = tid; i < R * F; i += NT) {
+  for (int i = tid; i < R * F; i += RNT) {
     const int r = i / F, c = i - r * F;
-    const float g = repa[i] > 0.f ? kcomb<R, 4>(red, F, r, c) : 0.f;
+    const float g = repa[i] > 0.f ? kcomb<R, RNT / 64>(red, F, r, c) : 0.f;
     if (valid(r)) s.g_rep[(size_t)(b0 + r) * F + c] = g;
   }
   if (tid < R && valid(tid)) {
@@ -565,7 +565,7 @@ __device__ __forceinline__ void adam(float* pp, float* mm, float* vv, size_t i, 
 }
 
 #ifndef MZT_NW2
-#define MZT_NW2 8
+#define MZT_NW2 16
 #endif
 constexpr int NW2 = MZT_NW2;  // waves per weight tile: they split the B*U rows
 __global__ __launch_bounds__(64 * NW2) void mzt_grad_adam_kernel(MztGradParams P) {
@@ -659,7 +659,7 @@ hipError_t launch_rows(const MztRowParams& p, hipStream_t stream) {
   auto kern = mzt_rows_kernel<R, SUP>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3((p.B + R - 1) / R), dim3(NT), smem, stream, p);
+  hipLaunchKernelGGL(kern, dim3((p.B + R - 1) / R), dim3(RNT), smem, stream, p);
   return hipGetLastError();
 }
 
