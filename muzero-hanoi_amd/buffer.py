@@ -60,8 +60,9 @@ class Buffer:
         return self.states[i], self.rwds[i], self.actions[i], self.pi_probs[i], self.mc_returns[i]
 
     def uniform_sample(self, batch_s):
-        """buffer.py:79-87"""
-        indx = np.random.choice(np.arange(len(self)), size=batch_s, replace=True).astype(np.int64)
+        """buffer.py:79-87.  np.random.choice(np.arange(n), batch_s, replace=True) draws
+        RandomState.randint(0, n, batch_s); the same call without building the index array."""
+        indx = np.random.randint(0, len(self), size=batch_s).astype(np.int64)
         return self._gather(indx)
 
     def priority_sample(self, batch_s):
@@ -69,7 +70,13 @@ class Buffer:
         num = len(self)
         p = self.priorities[:num] ** self._priority_exponent
         probs = p / np.sum(p)
-        indx = np.random.choice(np.arange(num), size=batch_s, replace=True, p=probs).astype(np.int64)
+        # np.random.choice(np.arange(num), batch_s, replace=True, p=probs) as RandomState.choice
+        # computes it -- float64 cdf, cdf /= cdf[-1], one random_sample per index, right-sided
+        # searchsorted -- without its input validation and index-array gather: the same indices
+        # from the same stream position (tests/test_training.py checks them against the reference)
+        cdf = probs.astype(np.float64).cumsum()
+        cdf /= cdf[-1]
+        indx = cdf.searchsorted(np.random.random_sample(batch_s), side="right").astype(np.int64)
         w = ((1.0 / self.size) / probs[indx]) ** self._importance_sampling_exponent
         w /= np.max(w)
         return (*self._gather(indx), indx, torch.from_numpy(w).to(self.dev, dtype=torch.float32))

@@ -286,6 +286,7 @@ class FusedUpdate:
                    for p in self.params[0::2]]
         self.scratch = None
         self.B = None
+        self._a = None
         self._seen = None  # parameter versions after our own last write
 
     def _versions(self):
@@ -301,50 +302,61 @@ class FusedUpdate:
                 st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
         return [opt.state[p] for p in self.params]
 
-    def _args(self, B):
+    def _setup(self, B, device):
+        """scratch / outputs for batch size B and the argument block's fixed pointers: parameters,
+        transposed copies and the optimiser's moment tensors (re-done when the optimiser's state
+        objects change, e.g. after load_state_dict)"""
         L = self._lib
+        U = self.mz.unroll_n_steps
+        if self.B != B:
+            nb = ctypes.c_size_t()
+            L.check(L.lib().mzh_train_scratch_bytes(B, U, self.in_dim, self.support, nb), "mzh_train_scratch_bytes")
+            self.scratch = torch.empty(nb.value // 4 + 64, dtype=torch.float32, device=device)
+            self.row_loss = torch.empty(B, 3, dtype=torch.float32, device=device)
+            self.new_prio = torch.empty(B, dtype=torch.float32, device=device)
+            self.B = B
+        states_ = self._state()
         a = L.TrainArgs()
-        a.B, a.U, a.in_dim, a.support, a.rows = B, self.mz.unroll_n_steps, self.in_dim, self.support, 0
+        a.B, a.U, a.in_dim, a.support, a.rows = B, U, self.in_dim, self.support, 0
         for i, p in enumerate(self.params):
             a.param[i] = p.data_ptr()
         for i, w in enumerate(self.wt):
             a.wt[i] = w.data_ptr()
-        return a
-
-    def __call__(self, states, rwds, actions, pi_probs, returns, priority_w):
-        L = self._lib
-        B, U = states.shape[0], self.mz.unroll_n_steps
-        stream = torch.cuda.current_stream().cuda_stream
-        if self.B != B:
-            nb = ctypes.c_size_t()
-            L.check(L.lib().mzh_train_scratch_bytes(B, U, self.in_dim, self.support, nb), "mzh_train_scratch_bytes")
-            self.scratch = torch.empty(nb.value // 4 + 64, dtype=torch.float32, device=states.device)
-            self.row_loss = torch.empty(B, 3, dtype=torch.float32, device=states.device)
-            self.new_prio = torch.empty(B, dtype=torch.float32, device=states.device)
-            self.B = B
-        a = self._args(B)
-        if self._seen != self._versions():  # parameters written outside this update: re-transpose
-            L.check(L.lib().mzh_train_transpose(a, stream), "mzh_train_transpose")
-        states_ = self._state()
-        g = self.mz.networks.optimiser.param_groups[0]
-        beta1, beta2 = g["betas"]
-        for st in states_:
-            st["step"] += 1
-        step = float(states_[0]["step"])
-        a.step_size = g["lr"] / (1 - beta1 ** step)
-        a.bc2_sqrt = math.sqrt(1 - beta2 ** step)
-        a.beta1, a.beta2, a.eps = beta1, beta2, g["eps"]
         for i, st in enumerate(states_):
             a.exp_avg[i] = st["exp_avg"].data_ptr()
             a.exp_avg_sq[i] = st["exp_avg_sq"].data_ptr()
+        a.scratch = self.scratch.data_ptr()
+        a.scratch_bytes = self.scratch.numel() * 4
+        a.row_loss = self.row_loss.data_ptr()
+        self._a = a
+        self._steps = [st["step"] for st in states_]
+        self._state_key = self._state_identity()
+
+    def _state_identity(self):
+        opt = self.mz.networks.optimiser
+        return (id(opt.state),) + tuple(id(opt.state[p].get("exp_avg")) for p in self.params)
+
+    def __call__(self, states, rwds, actions, pi_probs, returns, priority_w):
+        L = self._lib
+        B = states.shape[0]
+        stream = torch.cuda.current_stream().cuda_stream
+        if self._a is None or self.B != B or self._state_key != self._state_identity():
+            self._setup(B, states.device)
+        a = self._a
+        if self._seen != self._versions():  # parameters written outside this update: re-transpose
+            L.check(L.lib().mzh_train_transpose(a, stream), "mzh_train_transpose")
+        g = self.mz.networks.optimiser.param_groups[0]
+        beta1, beta2 = g["betas"]
+        torch._foreach_add_(self._steps, 1)  # Adam's per-parameter step counters (host tensors)
+        step = float(self._steps[0])
+        a.step_size = g["lr"] / (1 - beta1 ** step)
+        a.bc2_sqrt = math.sqrt(1 - beta2 ** step)
+        a.beta1, a.beta2, a.eps = beta1, beta2, g["eps"]
         ins = [states.float().contiguous(), rwds.float().contiguous(), actions.long().contiguous(),
                pi_probs.float().contiguous(), returns.float().contiguous()]
         w = priority_w.float().contiguous() if priority_w is not None else None
         a.obs, a.rwds, a.actions, a.pi, a.returns = (t.data_ptr() for t in ins)
         a.weights = w.data_ptr() if w is not None else None
-        a.scratch = self.scratch.data_ptr()
-        a.scratch_bytes = self.scratch.numel() * 4
-        a.row_loss = self.row_loss.data_ptr()
         a.new_prio = self.new_prio.data_ptr() if w is not None else None
         L.check(L.lib().mzh_train_update(a, stream), "mzh_train_update")
         for p in self.params:  # the kernel wrote the parameters in place: let version trackers know

@@ -136,3 +136,31 @@ def test_training_loop_runs_on_gpu():
     assert moved
     action, pi, q = mz.mcts.run_mcts(mz.env.reset(), mz.networks, temperature=1.0, deterministic=True)
     assert 0 <= action < 6 and abs(pi.sum() - 1) < 1e-9 and np.isfinite(q)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_sampling_fast_path_equals_numpy_choice(seed):
+    """Buffer's draw == np.random.choice(arange(n), size, replace=True[, p]) (buffer.py:79-112):
+    same indices and the same global-stream position afterwards, with and without priorities."""
+    from muzero_hanoi_amd.buffer import Buffer
+
+    g = np.random.default_rng(seed)
+    n = int(g.integers(1, 5000))
+    buf = Buffer(n, 5, d_state=9, n_action=6, device="cpu")
+    buf.priorities[:] = (g.random(n) + 0.01).astype(np.float32)
+    buf.ptr, buf.is_full = 0, True
+    probs = buf.priorities / np.sum(buf.priorities)
+    np.random.seed(seed)
+    want = np.random.choice(np.arange(n), size=64, replace=True, p=probs)
+    after = np.random.random_sample()
+    np.random.seed(seed)
+    got = buf.priority_sample(64)[5]
+    assert np.array_equal(got, want) and np.random.random_sample() == after
+    np.random.seed(seed)
+    want = np.random.choice(np.arange(n), size=64, replace=True)
+    after = np.random.random_sample()
+    np.random.seed(seed)
+    st = buf.uniform_sample(64)[0]
+    assert np.random.random_sample() == after and st.shape == (64, 9)
+    np.random.seed(seed)
+    assert np.array_equal(np.random.randint(0, n, size=64), want)
