@@ -24,6 +24,10 @@
 #ifndef MZW_PRIO
 #define MZW_PRIO 0    // ping-pong priority: 0 none, 1 static s_setprio(1) for waves 4-7, 2 M phases
 #endif
+#ifndef MZW_SPRIO
+#define MZW_SPRIO 2   // sequential schedule: 1 static s_setprio(1) for odd workgroups (one of the two
+                      // workgroups sharing each SIMD), 2 s_setprio(1) around every M phase
+#endif
 #ifndef MZW_PPBAR
 #define MZW_PPBAR 0   // slot barrier: 0 __syncthreads (drains memory), 1 bare s_barrier
 #endif
@@ -825,11 +829,14 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
 
   MZH_STAMP_DECL
   if (!MZW_PP) {
+    if (MZW_SPRIO == 1 && (blockIdx.x & 1)) __builtin_amdgcn_s_setprio(1);
     for (int s = 0; s < S; ++s) {
       MZH_STAMP(4);
       phase_select(s);
       MZH_STAMP(0);
+      if (MZW_SPRIO == 2) __builtin_amdgcn_s_setprio(1);
       phase_mlp(s);
+      if (MZW_SPRIO == 2) __builtin_amdgcn_s_setprio(0);
       MZH_STAMP(1);
       phase_head(s);
       MZH_STAMP(2);
