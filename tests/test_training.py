@@ -164,3 +164,52 @@ def test_sampling_fast_path_equals_numpy_choice(seed):
     assert np.random.random_sample() == after and st.shape == (64, 9)
     np.random.seed(seed)
     assert np.array_equal(np.random.randint(0, n, size=64), want)
+
+
+@pytest.mark.gpu
+def test_fused_update_after_checkpoint_reload():
+    """FusedUpdate re-transposes weights written outside it and re-binds the optimiser's state
+    tensors after `load_state_dict` (training_main.py:93-103 checkpoint format): an update right
+    after a reload matches the torch update from the same checkpoint."""
+    import copy
+
+    from muzero_hanoi_amd.muzero import Muzero
+
+    def make(impl):
+        torch.manual_seed(0)
+        return Muzero(env=None, s_space_size=9, n_action=6, discount=0.8, dirichlet_alpha=0.25, n_mcts_simulations=5,
+                      unroll_n_steps=5, batch_s=32, TD_return=True, n_TD_step=10, lr=0.002, buffer_size=200,
+                      priority_replay=True, device="cuda", update_impl=impl)
+
+    data = synthetic_transitions(3, 7, T=120)
+    fused, ref = make("fused"), make("torch")
+    for mz in (fused, ref):
+        mz.buffer.add(*data)
+    # a checkpoint taken after two torch updates
+    np.random.seed(5)
+    for _ in range(2):
+        s, r, a, p, ret, indx, w = ref.buffer.priority_sample(32)
+        ref._update(s, r, a, p, ret, w)
+    ckpt = {"Muzero_net": copy.deepcopy(ref.networks.state_dict()),
+            "Net_optim": copy.deepcopy(ref.networks.optimiser.state_dict())}
+    # the fused agent trains on its own first, then loads the checkpoint
+    np.random.seed(6)
+    for _ in range(2):
+        s, r, a, p, ret, indx, w = fused.buffer.priority_sample(32)
+        fused._update(s, r, a, p, ret, w)
+    fused.networks.load_state_dict(ckpt["Muzero_net"])
+    fused.networks.optimiser.load_state_dict(ckpt["Net_optim"])
+    np.random.seed(9)
+    batch = fused.buffer.priority_sample(32)
+    out_f = fused._update(*batch[:5], batch[6])
+    out_r = ref._update(*batch[:5], batch[6])
+    for x, y in zip(out_f[1:], out_r[1:]):
+        np.testing.assert_allclose(float(x), float(y), rtol=2e-4)
+    np.testing.assert_allclose(out_f[0], out_r[0], rtol=1e-3, atol=1e-3)
+    pf = torch.cat([v.reshape(-1) for v in fused.networks.state_dict().values()]).cpu().numpy()
+    pr = torch.cat([v.reshape(-1) for v in ref.networks.state_dict().values()]).cpu().numpy()
+    d = np.abs(pf - pr)
+    assert (d < 1e-5).mean() > 0.99 and d.max() < 6 * 0.002, (float((d < 1e-5).mean()), float(d.max()))
+    sf = fused.networks.optimiser.state_dict()["state"]
+    sr = ref.networks.optimiser.state_dict()["state"]
+    assert all(float(sf[i]["step"]) == float(sr[i]["step"]) == 3.0 for i in sr)
