@@ -177,13 +177,15 @@ class Engine:
 
 
 # ---------------------------------------------------------------- environment (no engine needed)
-def env_step(n_disks, max_steps, state, action, step_ctr, active, goal_peg=2, moved=None, obs=None, err=None):
-    """Batched TowersOfHanoi.step on device tensors (state/step_ctr/active updated in place)."""
+def env_step(n_disks, max_steps, state, action, step_ctr, active, goal_peg=2, moved=None, obs=None, err=None,
+             reward=None, done=None, illegal=None):
+    """Batched TowersOfHanoi.step on device tensors (state/step_ctr/active updated in place;
+    reward codes / done / illegal written to the given tensors or fresh ones)."""
     B = state.shape[0]
     dev = state.device
-    reward = torch.empty(B, dtype=torch.int8, device=dev)
-    done = torch.empty(B, dtype=torch.uint8, device=dev)
-    illegal = torch.empty(B, dtype=torch.uint8, device=dev)
+    reward = torch.empty(B, dtype=torch.int8, device=dev) if reward is None else reward
+    done = torch.empty(B, dtype=torch.uint8, device=dev) if done is None else done
+    illegal = torch.empty(B, dtype=torch.uint8, device=dev) if illegal is None else illegal
     check(_lib.lib().mzh_env_step(n_disks, goal_peg, max_steps, B, ptr(state), ptr(action), ptr(moved), ptr(obs),
                                   ptr(reward), ptr(done), ptr(illegal), ptr(step_ctr), ptr(active), ptr(err),
                                   _lib.stream_handle(dev)), "mzh_env_step")

@@ -15,6 +15,7 @@ import torch
 
 from . import engine
 from .engine import require_device
+from .staging import Packed
 
 _REWARD = {0: 0, 1: 100, -1: -100 / 1000}  # codes of mzh_env_step -> the reference's rewards
 
@@ -34,6 +35,7 @@ class TowersOfHanoi:
         self.reset_check = False
         self.step_counter = 0
         self._dev = torch.device("cuda", torch.cuda.current_device())
+        self._pk = None
 
     # ------------------------------------------------------------------ reference API
     def step(self, action):
@@ -42,21 +44,22 @@ class TowersOfHanoi:
         action = int(action)
         if not 0 <= action < 6:
             raise IndexError("list index out of range")
-        dev = self._dev
-        st = torch.tensor([list(self.c_state)], dtype=torch.uint8, device=dev)
-        moved = torch.empty_like(st)
-        obs = torch.empty((1, self.oneH_s_size), dtype=torch.float32, device=dev)
-        ctr = torch.tensor([self.step_counter], dtype=torch.int32, device=dev)
-        active = torch.ones(1, dtype=torch.uint8, device=dev)
-        code, done, illegal = engine.env_step(self.discs, self.max_steps, st, torch.tensor([action], dtype=torch.int32, device=dev),
-                                              ctr, active, goal_peg=self.goal_peg, moved=moved, obs=obs)
-        host = torch.cat([st[0].to(torch.int32), ctr, active.to(torch.int32), code.to(torch.int32),
-                          done.to(torch.int32), illegal.to(torch.int32)]).cpu().tolist()
-        n = self.discs
-        self.c_state = tuple(host[:n])
-        self.step_counter, self.reset_check = host[n], bool(host[n + 1])
-        rwd, done_b, illegal_b = _REWARD[host[n + 2]], bool(host[n + 3]), bool(host[n + 4])
-        return obs[0].to(torch.float64).cpu().numpy(), rwd, done_b, illegal_b
+        # inputs down in one copy, the kernel, every output back in one copy (staging.Packed)
+        pk = self._packed()
+        h, d = pk.h, pk.d
+        h["state"][0] = self.c_state
+        h["action"][0] = action
+        h["ctr"][0] = self.step_counter
+        h["active"][0] = 1
+        pk.to_device()
+        engine.env_step(self.discs, self.max_steps, d["state"], d["action"], d["ctr"], d["active"],
+                        goal_peg=self.goal_peg, moved=d["moved"], obs=d["obs"], reward=d["code"], done=d["done"],
+                        illegal=d["illegal"])
+        pk.to_host()
+        self.c_state = tuple(int(x) for x in h["state"][0])
+        self.step_counter, self.reset_check = int(h["ctr"][0]), bool(h["active"][0])
+        rwd, done_b, illegal_b = _REWARD[int(h["code"][0])], bool(h["done"][0]), bool(h["illegal"][0])
+        return h["obs"][0].astype(np.float64), rwd, done_b, illegal_b
 
     def reset(self):
         self.reset_check = True
@@ -86,6 +89,16 @@ class TowersOfHanoi:
         return bool((int(mask.item()) >> self.moves.index(tuple(move))) & 1)
 
     # ------------------------------------------------------------------ helpers
+    def _packed(self):
+        if self._pk is None:
+            n = self.discs
+            self._pk = Packed([("state", torch.uint8, (1, n)), ("action", torch.int32, (1,)),
+                               ("ctr", torch.int32, (1,)), ("active", torch.uint8, (1,)),
+                               ("moved", torch.uint8, (1, n)), ("obs", torch.float32, (1, 3 * n)),
+                               ("code", torch.int8, (1,)), ("done", torch.uint8, (1,)),
+                               ("illegal", torch.uint8, (1,))], self._dev)
+        return self._pk
+
     def _encode(self, state):
         st = torch.tensor([list(state)], dtype=torch.uint8, device=self._dev)
         return engine.encode_obs(self.discs, st)[0].to(torch.float64).cpu().numpy()

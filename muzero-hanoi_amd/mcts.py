@@ -16,6 +16,7 @@ import torch
 
 from . import rng as _rng
 from .networks import engine_for
+from .staging import Packed
 
 
 _REPLAY_ENGINES = {}
@@ -101,17 +102,30 @@ class MCTS:
         else:
             eng = engine_for(network, S, 1)
         dev = eng.device
-        obs = torch.as_tensor(np.asarray(state)).to(dev, torch.float32).reshape(1, -1)
-        mm = torch.tensor([[self.min_max_stats.maximum, self.min_max_stats.minimum]], dtype=torch.float64, device=dev)
-        t = lambda a: None if a is None else torch.from_numpy(np.asarray(a)).to(dev)
-        out = eng.search(S, obs=None if replay else obs, replay=replay, tie_idx=t(tie), noise=t(noise), action_u=t(u),
-                         minmax_in=mm, temperature=float(temperature), deterministic=bool(deterministic),
-                         discount=float(self.discount), eps=float(self.root_exploration_eps), np1_ucb=self.np1_ucb)
-        host = {k: v.cpu().numpy() for k, v in out.items() if k != "_keep"}
+        x = np.asarray(state).reshape(-1)
+        # inputs down in one copy, every output back in one copy (staging.Packed)
+        pin, pout = self._packed(eng, S, x.size, replay is not None)
+        h = pin.h
+        h["obs"][0] = x
+        h["mm"][0] = (self.min_max_stats.maximum, self.min_max_stats.minimum)
+        h["tie"][:] = tie
+        if noise is not None:
+            h["noise"][:] = noise
+        if u is not None:
+            h["u"][:] = u
+        pin.to_device()
+        d = pin.d
+        out = eng.search(S, obs=None if replay else d["obs"], replay=replay, tie_idx=d["tie"],
+                         noise=None if noise is None else d["noise"], action_u=None if u is None else d["u"],
+                         minmax_in=d["mm"], temperature=float(temperature), deterministic=bool(deterministic),
+                         discount=float(self.discount), eps=float(self.root_exploration_eps), np1_ucb=self.np1_ucb,
+                         out=dict(pout.d))
+        pout.to_host()
+        host = pout.h
         self.min_max_stats.maximum = float(host["minmax"][0, 0])
         self.min_max_stats.minimum = float(host["minmax"][0, 1])
         L = int(host["latent_len"][0])
-        self.latent_actions = [torch.tensor([int(m)], dtype=torch.long, device=self.dev) for m in host["latent"][0, :L]]
+        self._latent_host = [int(m) for m in host["latent"][0, :L]]  # tensors made on first access
         self.last_extra_ties = int(host["extra_ties"][0])
         if self.last_extra_ties:
             warnings.warn("search met an argmax tie beyond the root's first selection: the NumPy RNG stream "
@@ -120,6 +134,34 @@ class MCTS:
 
     def return_latent_actions(self):
         return self.latent_actions
+
+    @property
+    def latent_actions(self):
+        """mcts.py:79, 84-86: the last simulation's path as [LongTensor[1]] on the MCTS device"""
+        if self._latent_host is not None:
+            self._latent = [torch.tensor([m], dtype=torch.long, device=self.dev) for m in self._latent_host]
+            self._latent_host = None
+        return self._latent
+
+    @latent_actions.setter
+    def latent_actions(self, value):
+        self._latent = value
+        self._latent_host = None
+
+    def _packed(self, eng, S, in_dim, replay):
+        key = (id(eng), S, in_dim, replay)
+        if getattr(self, "_pk_key", None) != key:
+            dev = eng.device
+            self._pk_in = Packed([("obs", torch.float32, (1, in_dim)), ("noise", torch.float64, (1, 6)),
+                                  ("tie", torch.int32, (1,)), ("u", torch.float64, (1,)),
+                                  ("mm", torch.float64, (1, 2))], dev)
+            self._pk_out = Packed([("visits", torch.int32, (1, 6)), ("root_q", torch.float64, (1,)),
+                                   ("minmax", torch.float64, (1, 2)), ("extra_ties", torch.int32, (1,)),
+                                   ("action", torch.int32, (1,)), ("pi", torch.float64, (1, 6)),
+                                   ("latent", torch.int32, (1, S + 1)), ("latent_len", torch.int32, (1,)),
+                                   ("sel_steps", torch.int32, (1,))], dev)
+            self._pk_key = key
+        return self._pk_in, self._pk_out
 
     def add_dirichlet_noise(self, prob, eps=0.25, alpha=0.25):
         """mcts.py:132-152 (host form, for callers that use it directly)."""
