@@ -359,7 +359,9 @@ extern "C" int mzh_hanoi_solver(int n_disks, int goal_peg, int B, const uint8_t*
 }
 
 // ---- inference ----
-// roots (rows) per workgroup: 32 when that still gives >= 256 workgroups, else 16.
+// roots (rows) per workgroup: 16 while that fits one workgroup per CU (B <= 4096), else 32 -- a
+// second round of 16-row workgroups costs more than the 32-row tiles (measured: 5,120 roots 1.05e8
+// vs 1.68e8 sims/s, 7,168 roots 1.46e8 vs 2.32e8; 4,096 roots 1.58e8 vs 1.34e8).
 // MZH_ROWS=16|32 in the environment forces a tile size (A/B experiments only).
 static int pick_rows(int B) {
   static const int forced = [] {
@@ -367,7 +369,7 @@ static int pick_rows(int B) {
     return v ? atoi(v) : 0;
   }();
   if (forced == 16 || forced == 32) return forced;
-  return B >= 256 * 32 ? 32 : 16;
+  return B > 256 * 16 ? 32 : 16;
 }
 
 extern "C" int mzh_initial_inference(mzh_engine* eng, int B, const float* obs, float* h, float* reward, float* pi,

@@ -138,10 +138,13 @@ __device__ __forceinline__ double mzh_pow(double x, double e) {
 
 // R = 32: one workgroup per CU (all 512 registers per lane); R = 16: two co-resident workgroups
 // per CU (<= 256 registers), so one workgroup's latency-bound tree phase overlaps the other's MFMAs.
+#ifndef MZH_PF16
+#define MZH_PF16 1  // 1: R = 16 also prefetches across the tree phase (needs the full register file: one workgroup per CU)
+#endif
 template <int R, bool REPLAY, bool OHL>
-__global__ __launch_bounds__(MZH_THREADS, R == 16 ? 2 : 1) void mzh_search_kernel(MzhNet net, MzhSearchParams p) {
+__global__ __launch_bounds__(MZH_THREADS, R == 16 && !MZH_PF16 ? 2 : 1) void mzh_search_kernel(MzhNet net, MzhSearchParams p) {
   constexpr int DC = SearchSmem<R>::DC;
-  constexpr bool PF = R == 32;  // keep the next step's first weight chunks in flight across the tree phase
+  constexpr bool PF = R == 32 || MZH_PF16;  // keep the next step's first weight chunks in flight across the tree phase
   extern __shared__ __align__(16) unsigned char smem_raw[];
   MlpSmem<R>& sm = *reinterpret_cast<MlpSmem<R>*>(smem_raw);
   SearchSmem<R>& st = *reinterpret_cast<SearchSmem<R>*>(smem_raw + sizeof(MlpSmem<R>));
