@@ -179,7 +179,7 @@ def main():
     value = sims_total / dt
     flops_launch = B * (S * MLP_FLOP_PER_SIM + root_flops(N))
     achieved = flops_launch / (kern_ms * 1e-3) / 1e12
-    kern_sel = a.kernel if a.kernel != "auto" else ("wave" if B >= 53248 else "wave16" if B >= 12288 else "coop")
+    kern_sel = a.kernel if a.kernel != "auto" else ("wave" if B >= 53248 else "wave16" if B > 8192 else "coop")
     coop_rows = 32 if B > 4096 else 16  # mzh_api.hip choose_kernel() / pick_rows()
     kernel_name = {"wave": "mzh_wave_kernel<2,false,true>", "wave16": "mzh_wave_kernel<1,false,true>",
                    "coop": f"mzh_search_kernel<{coop_rows},false,*>"}[kern_sel]

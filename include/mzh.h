@@ -44,7 +44,7 @@ extern "C" {
                                U = fl32(fl64(prior * w)); default is NumPy 2: fl32(prior * fl32(w)) */
 #define MZH_FLAG_KERNEL_COOP 2u /* force the cooperative kernel (4 waves share one 32-root tile) */
 #define MZH_FLAG_KERNEL_WAVE 4u /* force the wave-independent kernel, 32 roots per wave (default for B >= 53248) */
-#define MZH_FLAG_KERNEL_WAVE16 8u /* force the wave-independent kernel, 16 roots per wave (default for 12288 <= B < 53248) */
+#define MZH_FLAG_KERNEL_WAVE16 8u /* force the wave-independent kernel, 16 roots per wave (default for 8192 < B < 53248) */
 
 typedef struct mzh_engine mzh_engine;
 typedef void* mzh_stream; /* hipStream_t */

@@ -411,7 +411,7 @@ static const size_t kMaxLds = 163840;
 // gives >= 1024 waves (one per SIMD, two co-resident per SIMD at 65k roots), with 16 roots per wave
 // for mid-size batches (>= 1024 such waves), else the cooperative kernel (mzh_search.hip) whose 4
 // waves share one 32-root MLP tile.  MZH_FLAG_KERNEL_* (or MZH_KERNEL=coop|wave|wave16) force one.
-static const int kWaveMinRoots = 53248, kWave16MinRoots = 12288;  // measured crossovers
+static const int kWaveMinRoots = 53248, kWave16MinRoots = 8193;  // measured crossovers
 struct KernelChoice {
   bool wave;
   int nt;  // wave kernel: 16-root column tiles per wave
