@@ -92,6 +92,46 @@ def cpu_baseline(n_disks, S, seconds, seed):
                       f"MCTS/mcts.py + networks.py and matches the reference's visits bit-exactly"}
 
 
+def cpu_baseline_selfplay(n_disks, S, max_steps, seconds, net_state, start_state):
+    """Self-play CPU baseline (tools/bench_selfplay.py): the reference algorithm on one host core --
+    oracle/py_port.py's object-tree MCTS (batch-1 torch-CPU MLP, NumPy RNG) and the C env
+    restatement -- playing episodes from start_state(k) until done or `seconds` run out.
+    Returns (decisions, episodes, seconds)."""
+    from oracle import oracle as orc
+    from oracle import py_port
+
+    torch.set_num_threads(1)
+    pnet = py_port.PortNet({k: v.detach().cpu().numpy() for k, v in net_state.items()})
+    np.random.seed(4)
+    moves, eps_done = 0, 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        idx = int(start_state(eps_done))
+        st = np.array([(idx // 3 ** (n_disks - 1 - d)) % 3 for d in range(n_disks)], np.uint8)
+        ctr, active, done = 0, 1, 0
+        mcts = py_port.PortMCTS(0.8, 0.25, S)  # one instance per game, as Muzero keeps one
+        while not done and time.perf_counter() - t0 < seconds:
+            obs = np.zeros(3 * n_disks)
+            obs[np.arange(n_disks) * 3 + st] = 1.0
+            action = mcts.run_mcts(obs, pnet, 1.0, False)[0]
+            _, st, _, ctr, active, done, _ = orc.env_step(st, action, ctr, active, max_steps)
+            moves += 1
+        eps_done += 1
+    return moves, eps_done, time.perf_counter() - t0
+
+
+def cpu_baseline_solver(states, seconds):
+    """hanoi_solver CPU baseline (tools/bench_eval.py): the C restatement (oracle/mzh_oracle.c) on
+    one host core over a prefix of `states`.  Returns (moves of the prefix, states/s)."""
+    from oracle import oracle as orc
+
+    ref, k, t0 = [], 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds and k < len(states):
+        ref.append(orc.hanoi_solver(states[k]))
+        k += 1
+    return np.array(ref, np.int32), k / (time.perf_counter() - t0)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -7,7 +7,7 @@ count from hanoi_solver (env/hanoi_utils.py:4-26), and the illegal-move rate
 Legs:
   evaluate     selfplay.evaluate on the GPU: every start of a budget in one lockstep batch
   solver       device hanoi_solver over 2^20 random states (N=7) vs the C restatement on one host
-               core (oracle/mzh_oracle.c, bounded sample)
+               core (bench.cpu_baseline_solver, bounded sample)
 
   python tools/bench_eval.py [--starts 4096] [--budgets 1,5,10,25,50]
 """
@@ -36,7 +36,8 @@ def main():
     from muzero_hanoi_amd.engine import hanoi_solver_batch
     from muzero_hanoi_amd.networks import MuZeroNet
     from muzero_hanoi_amd.selfplay import evaluate
-    from oracle import oracle as orc
+
+    from bench import cpu_baseline_solver
 
     recs = []
     torch.manual_seed(1)
@@ -68,13 +69,9 @@ def main():
         out = hanoi_solver_batch(n, dst)
     torch.cuda.synchronize()
     gpu = reps * a.solver_states / (time.perf_counter() - t0)
-    k, t0 = 0, time.perf_counter()
-    ref = []
-    while time.perf_counter() - t0 < a.cpu_seconds and k < a.solver_states:
-        ref.append(orc.hanoi_solver(st[k]))
-        k += 1
-    cpu = k / (time.perf_counter() - t0)
-    same = bool(np.array_equal(out[:k].cpu().numpy(), np.array(ref, np.int32)))
+    ref, cpu = cpu_baseline_solver(st, a.cpu_seconds)
+    k = len(ref)
+    same = bool(np.array_equal(out[:k].cpu().numpy(), ref))
     recs.append({"leg": "solver", "metric": "hanoi_solver_states_per_sec", "value": gpu, "unit": "states/s",
                  "cpu_baseline": {"value": cpu, "unit": "states/s", "cores": 1, "kind": "port",
                                   "sample": f"{k} states through oracle/mzh_oracle.c via ctypes"},

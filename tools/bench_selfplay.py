@@ -9,8 +9,9 @@ Legs:
             env-kernel launch per move over every unfinished episode)
   drop-in   the reference's sequential loop through the drop-ins (selfplay.play_game: one
             MCTS.run_mcts launch and one env.step per decision, as Muzero._play_game runs it)
-  cpu       the reference algorithm on one host core: oracle/py_port.py's object-tree MCTS with a
-            batch-1 torch-CPU MLP + the C env restatement, bounded to --cpu-seconds
+  cpu       the reference algorithm on one host core (bench.cpu_baseline_selfplay: oracle/py_port.py's
+            object-tree MCTS with a batch-1 torch-CPU MLP + the C env restatement), bounded to
+            --cpu-seconds
 
   python tools/bench_selfplay.py [--legs batched,drop-in,cpu] [--episodes 4096] [--sims 25]
 """
@@ -68,27 +69,11 @@ def leg_dropin(args, net):
 
 
 def leg_cpu(args, net):
-    from oracle import oracle as orc
-    from oracle import py_port
+    from bench import cpu_baseline_selfplay
 
-    torch.set_num_threads(1)
-    pnet = py_port.PortNet({k: v.detach().cpu().numpy() for k, v in net.state_dict().items()})
-    np.random.seed(4)
-    moves, eps_done = 0, 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < args.cpu_seconds:
-        idx = int(start_states(args.disks, 1, 200 + eps_done)[0])
-        st = np.array([(idx // 3 ** (args.disks - 1 - d)) % 3 for d in range(args.disks)], np.uint8)
-        ctr, active, done = 0, 1, 0
-        mcts = py_port.PortMCTS(0.8, 0.25, args.sims)  # one instance per game, as Muzero keeps one
-        while not done and time.perf_counter() - t0 < args.cpu_seconds:
-            obs = np.zeros(3 * args.disks)
-            obs[np.arange(args.disks) * 3 + st] = 1.0
-            action = mcts.run_mcts(obs, pnet, 1.0, False)[0]
-            _, st, _, ctr, active, done, _ = orc.env_step(st, action, ctr, active, args.max_steps)
-            moves += 1
-        eps_done += 1
-    dt = time.perf_counter() - t0
+    moves, eps_done, dt = cpu_baseline_selfplay(args.disks, args.sims, args.max_steps, args.cpu_seconds,
+                                                net.state_dict(),
+                                                lambda k: start_states(args.disks, 1, 200 + k)[0])
     return dict(decisions=moves, episodes=eps_done, seconds=dt, cores=1)
 
 
