@@ -316,3 +316,61 @@ def test_selftest_register_reciprocal(mzh):
     _lib.check(_lib.lib().mzh_selftest(_lib.MZH_SELFTEST_RCP, 1 << 20, _lib.ptr(bad), _lib.stream_handle(bad.device)),
                "mzh_selftest")
     assert int(bad.item()) == 0
+
+
+# ------------------------------------------------------- BASELINE.json configs at full size
+def _sample_idx(B, seed):
+    """first 16, last 16 and 16 random roots of a batch"""
+    mid = np.random.default_rng(seed).choice(np.arange(16, B - 16), 16, replace=False)
+    return np.unique(np.r_[0:16, np.sort(mid), B - 16:B])
+
+
+@pytest.mark.parametrize("B,S,n", [(4096, 50, 4),     # configs[1]
+                                   (16384, 200, 4),   # configs[3]
+                                   (32768, 100, 7),   # configs[4], one of its 8 shards
+                                   (65536, 50, 4)])   # the metric's batch (bench.py, per GPU)
+def test_search_baseline_configs_full_size(mzh, oracle, B, S, n):
+    """Each BASELINE.json search config at its full per-GPU size through the kernel the engine picks
+    for it: every root's visits sum to S, root Q is finite, and a sample of 48 roots (both ends of
+    the batch + 16 random) equals the oracle bit for bit (visits, root Q, action, selection steps)."""
+    flat, in_dim, sup = _weights(oracle, f"weights_N{n}_s0")
+    obs, noise, tie, u = _random_search_inputs(B, n, 1000 + B + S)
+    eng = _engine(mzh, n, S, B, sup, flat)
+    tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
+    o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0)
+    o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+    assert np.all(o["visits"].sum(1) == S)
+    assert np.all(np.isfinite(o["root_q"]))
+    assert np.all(o["sel_steps"] >= S)  # every simulation descends at least one edge
+    idx = _sample_idx(B, B + S)
+    ref = oracle.search(n, S, obs[idx], flat=flat, support=sup, noise=noise[idx], tie_idx=tie[idx],
+                        action_u=u[idx], temperature=1.0)
+    assert np.array_equal(o["visits"][idx], ref["visits"])
+    assert np.array_equal(o["root_q"][idx], ref["rootQ"])
+    assert np.array_equal(o["action"][idx], ref["action"])
+    assert np.array_equal(o["sel_steps"][idx], ref["sel_steps"])
+
+
+@pytest.mark.parametrize("B,S,n,W", [(65536, 50, 4, 8),    # configs[2]: 65,536 roots over 8 GPUs
+                                     (262144, 100, 7, 8)])  # configs[4]: 262,144 roots over 8 GPUs
+def test_search_sharded_equals_whole_batch(mzh, oracle, B, S, n, W):
+    """The multi-GPU decomposition (bench.py / distributed.py: rank r searches roots
+    [r*B/W, (r+1)*B/W) with the draws made in global root order) gives the same outputs as one
+    launch over the whole batch, bit for bit, although shard and whole batch run different
+    kernels (8,192-root shards: cooperative; 65,536 / 262,144 roots: wave)."""
+    flat, in_dim, sup = _weights(oracle, f"weights_N{n}_s0")
+    obs, noise, tie, u = _random_search_inputs(B, n, 2000 + B + S)
+    tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
+    eng = _engine(mzh, n, S, B, sup, flat)
+    whole = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0)
+    whole = {k: v.cpu().numpy() for k, v in whole.items() if k != "_keep"}
+    eng.close()
+    shard = B // W
+    es = _engine(mzh, n, S, shard, sup, flat)
+    for r in range(W):
+        sl = slice(r * shard, (r + 1) * shard)
+        o = es.search(S, obs=tt(obs[sl]), tie_idx=tt(tie[sl]), noise=tt(noise[sl]), action_u=tt(u[sl]),
+                      temperature=1.0)
+        o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+        for k in ("visits", "root_q", "pi", "action", "sel_steps", "minmax", "extra_ties"):
+            assert np.array_equal(o[k], whole[k][sl], equal_nan=True), (r, k)
