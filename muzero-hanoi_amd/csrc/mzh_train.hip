@@ -27,7 +27,7 @@
 
 namespace {
 
-constexpr int H = 64, F = 256, A = 6, NT = 256;
+constexpr int H = 64, F = 256, A = 6;
 
 // all-lane wave reductions without LDS: DPP within rows of 16 (xor 1, xor 2, half-mirror, mirror),
 // then v_permlane16_swap / v_permlane32_swap across rows
