@@ -62,6 +62,10 @@
 #ifndef MZW_SELPF
 #define MZW_SELPF 0   // selection: prefetch every child's block (towards L1) one level ahead
 #endif
+#ifndef MZW_SWP
+#define MZW_SWP 0     // MLP chains: layer 2 of hidden block ht-1 issued after layer 1 of block ht (hides the
+                      // acc -> ReLU -> layer-2 dependency; same k order, bit-identical)
+#endif
 #ifndef MZW_FENCE
 #define MZW_FENCE 1   // 1: workgroup-scope fence at the end of each simulation, 0: wavefront scope
 #endif
@@ -179,9 +183,102 @@ __device__ __forceinline__ double mzw_rcp(int n, const double* inv) { return MZW
 // wave's 2 column tiles.  x[n][kb] = the B operand of column tile n, k-block kb (lane group g
 // holds inputs 16kb + 4t + g, t = 0..3).  out[ot][n]: C registers of output tile ot.
 // ------------------------------------------------------------------------------------------
+// Software-pipelined form (MZW_SWP): iteration ht issues layer 1 of hidden block ht, then layer 2
+// of block ht-1 (its ReLU output computed one iteration earlier), then block ht's ReLU, so the
+// MFMA pipe never waits on acc -> bias/ReLU -> layer 2.  Every dot product keeps its k order
+// (layer 2 still accumulates block ht-1 before block ht).  Weight slots: w[0..KB1) roll layer-1
+// fragments one block ahead; w[KB1..FR) hold the layer-2 fragments of the block whose layer 2 is
+// next, refilled right after use; in the last iteration the layer-1 slots take block 15's layer-2
+// fragments (instead of the zero pad) so the epilogue's loads were issued a whole layer-1 earlier.
+template <int NT, int KB1, int NO, bool OH, bool LAST>
+__device__ __forceinline__ void mzw_swp_iter(int ht, const floatx4* S, floatx4 (&w)[KB1 + NO], const float* B1,
+                                             const floatx4 (&x)[NT][4], const float* const (&oh)[NT],
+                                             floatx4 (&hprev)[NT], floatx4 (&out)[NO][NT]) {
+  constexpr int FR = KB1 + NO;
+  const floatx4* Sn = S + (ht + 1) * FR * 64;
+  const floatx4* Sc = S + ht * FR * 64;
+  const floatx4 b = *reinterpret_cast<const floatx4*>(B1 + 16 * ht);
+  floatx4 o[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n)
+    o[n] = OH ? *reinterpret_cast<const floatx4*>(oh[n] + 16 * ht) : floatx4{0.f, 0.f, 0.f, 0.f};
+  floatx4 acc[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kb = 0; kb < KB1; ++kb) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[kb][t], x[n][kb][t], acc[n], 0, 0, 0);
+    if (!LAST)
+      w[kb] = Sn[kb * 64];
+    else if (kb < NO)
+      w[kb] = Sc[(KB1 + kb) * 64];  // block 15's layer-2 fragment ot = kb, for the epilogue
+    if (MZW_PIN) __builtin_amdgcn_sched_barrier(0);
+  }
+  if (ht > 0) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int ot = 0; ot < NO; ++ot)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+          out[ot][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[KB1 + ot][t], hprev[n][t], out[ot][n], 0, 0, 0);
+    if (!LAST) {
+#pragma unroll
+      for (int ot = 0; ot < NO; ++ot) w[KB1 + ot] = Sc[(KB1 + ot) * 64];
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = acc[n][i];
+      if (OH) v = v + o[n][i];  // one-hot action column (k = 64 + a)
+      v = v + b[i];
+      hprev[n][i] = v > 0.0f ? v : 0.0f;
+    }
+  }
+  if (MZW_PIN) __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int NT, int KB1, int NO, bool OH>
+__device__ __forceinline__ void mzw_chain_swp(const MzhWMlp& L, const floatx4 (&x)[NT][4],
+                                              const float* const (&oh)[NT], floatx4 (&out)[NO][NT], int lane) {
+  constexpr int FR = KB1 + NO;
+  const int g = lane >> 4;
+  const floatx4* S = reinterpret_cast<const floatx4*>(L.s) + lane;
+  const float* B1 = L.b1 + 4 * g;
+#pragma unroll
+  for (int ot = 0; ot < NO; ++ot)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) out[ot][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+  floatx4 w[FR];
+#pragma unroll
+  for (int f = 0; f < FR; ++f) w[f] = S[f * 64];
+  floatx4 hprev[NT];
+  MZW_UNROLL_PRAGMA
+  for (int ht = 0; ht < 15; ++ht) mzw_swp_iter<NT, KB1, NO, OH, false>(ht, S, w, B1, x, oh, hprev, out);
+  mzw_swp_iter<NT, KB1, NO, OH, true>(15, S, w, B1, x, oh, hprev, out);
+  // epilogue: layer 2 of block 15 (fragments in the layer-1 slots, see mzw_swp_iter)
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int ot = 0; ot < NO; ++ot)
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+        out[ot][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[ot][t], hprev[n][t], out[ot][n], 0, 0, 0);
+}
+
 template <int NT, int KB1, int NO, bool OH>
 __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[NT][4], const float* const (&oh)[NT],
                                           floatx4 (&out)[NO][NT], int lane) {
+  if constexpr (MZW_SWP && KB1 >= NO) {
+    mzw_chain_swp<NT, KB1, NO, OH>(L, x, oh, out, lane);
+    return;
+  }
   constexpr int FR = KB1 + NO;
   const int g = lane >> 4;
   const floatx4* S = reinterpret_cast<const floatx4*>(L.s) + lane;
