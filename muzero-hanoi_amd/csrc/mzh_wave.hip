@@ -66,6 +66,10 @@
 #define MZW_SWP 0     // MLP chains: layer 2 of hidden block ht-1 issued after layer 1 of block ht (hides the
                       // acc -> ReLU -> layer-2 dependency; same k order, bit-identical)
 #endif
+#ifndef MZW_PARK
+#define MZW_PARK 0    // park the root lanes' tree statistics in LDS across each M phase (3 instead of 6
+                      // VGPRs spilled, but neutral: 4.46e8 vs 4.47e8 sims/s over three A/B rounds)
+#endif
 #ifndef MZW_FENCE
 #define MZW_FENCE 1   // 1: workgroup-scope fence at the end of each simulation, 0: wavefront scope
 #endif
@@ -96,6 +100,11 @@ struct MzwWave {
   float pcR[MZW_DC][ROOTS];
   int pcN[MZW_DC][ROOTS];
   uint16_t path[MZW_DC][ROOTS];  // slot = parent expanded index * 8 + child
+#if MZW_PARK
+  // a root lane's tree statistics while its wave runs an M phase
+  double kd[5][ROOTS];
+  int ki[7][ROOTS];
+#endif
 };
 
 static __host__ __device__ inline size_t mzw_hdr_bytes(int S) {
@@ -924,6 +933,48 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
     }
   };
 
+  // MZW_PARK: the root lanes' statistics go to LDS before the M phase and come back after it; the
+  // compiler barrier between makes the reloads real, so none of these values is live (in VGPRs)
+  // across the MLP chains
+  auto park = [&]() {
+#if MZW_PARK
+    if (lane < ROOTS) {
+      ws.kd[0][rho] = mmax;
+      ws.kd[1][rho] = mmin;
+      ws.kd[2][rho] = den;
+      ws.kd[3][rho] = dinv;
+      ws.kd[4][rho] = rootW;
+      ws.ki[0][rho] = rootN;
+      ws.ki[1][rho] = firstTie;
+      ws.ki[2][rho] = extra;
+      ws.ki[3][rho] = steps;
+      ws.ki[4][rho] = depth;
+      ws.ki[5][rho] = leafE;
+      ws.ki[6][rho] = leafA;
+    }
+    asm volatile("" ::: "memory");
+#endif
+  };
+  auto unpark = [&]() {
+#if MZW_PARK
+    asm volatile("" ::: "memory");
+    if (lane < ROOTS) {
+      mmax = ws.kd[0][rho];
+      mmin = ws.kd[1][rho];
+      den = ws.kd[2][rho];
+      dinv = ws.kd[3][rho];
+      rootW = ws.kd[4][rho];
+      rootN = ws.ki[0][rho];
+      firstTie = ws.ki[1][rho];
+      extra = ws.ki[2][rho];
+      steps = ws.ki[3][rho];
+      depth = ws.ki[4][rho];
+      leafE = ws.ki[5][rho];
+      leafA = ws.ki[6][rho];
+    }
+#endif
+  };
+
   MZH_STAMP_DECL
   if (!MZW_PP) {
     if (MZW_SPRIO == 1 && (blockIdx.x & 1)) __builtin_amdgcn_s_setprio(1);
@@ -931,9 +982,11 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
       MZH_STAMP(4);
       phase_select(s);
       MZH_STAMP(0);
+      if (MZW_PARK) park();
       if (MZW_SPRIO == 2) __builtin_amdgcn_s_setprio(1);
       phase_mlp(s);
       if (MZW_SPRIO == 2) __builtin_amdgcn_s_setprio(0);
+      if (MZW_PARK) unpark();
       MZH_STAMP(1);
       phase_head(s);
       MZH_STAMP(2);
