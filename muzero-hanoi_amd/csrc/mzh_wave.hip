@@ -70,6 +70,11 @@
 #define MZW_PARK 0    // park the root lanes' tree statistics in LDS across each M phase (3 instead of 6
                       // VGPRs spilled, but neutral: 4.46e8 vs 4.47e8 sims/s over three A/B rounds)
 #endif
+#ifndef MZW_LAUNDER
+#define MZW_LAUNDER 0 // hide each chain's weight base pointer from the optimiser, so the chains' loads of
+                      // loop-invariant weight fragments are not hoisted out of the simulation loop (which
+                      // kept them live in VGPRs through the tree phases: 256 VGPRs + spills without it)
+#endif
 #ifndef MZW_FENCE
 #define MZW_FENCE 1   // 1: workgroup-scope fence at the end of each simulation, 0: wavefront scope
 #endif
@@ -187,6 +192,12 @@ __device__ __forceinline__ double mzw_rcp_reg(int n) {
 __device__ __forceinline__ double mzw_rcp(int n, const double* inv) { return MZW_RCP ? mzw_rcp_reg(n) : inv[n]; }
 
 
+// an SGPR pointer the optimiser cannot see through (MZW_LAUNDER)
+__device__ __forceinline__ const float4* mzw_opaque(const float4* q) {
+  if (MZW_LAUNDER) asm volatile("" : "+s"(q));
+  return q;
+}
+
 // ------------------------------------------------------------------------------------------
 // One MLP (layer1 + bias (+ one-hot column) + ReLU -> layer2, bias2 left to the caller) for the
 // wave's 2 column tiles.  x[n][kb] = the B operand of column tile n, k-block kb (lane group g
@@ -258,7 +269,7 @@ __device__ __forceinline__ void mzw_chain_swp(const MzhWMlp& L, const floatx4 (&
                                               const float* const (&oh)[NT], floatx4 (&out)[NO][NT], int lane) {
   constexpr int FR = KB1 + NO;
   const int g = lane >> 4;
-  const floatx4* S = reinterpret_cast<const floatx4*>(L.s) + lane;
+  const floatx4* S = reinterpret_cast<const floatx4*>(mzw_opaque(L.s)) + lane;
   const float* B1 = L.b1 + 4 * g;
 #pragma unroll
   for (int ot = 0; ot < NO; ++ot)
@@ -290,7 +301,7 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[N
   }
   constexpr int FR = KB1 + NO;
   const int g = lane >> 4;
-  const floatx4* S = reinterpret_cast<const floatx4*>(L.s) + lane;
+  const floatx4* S = reinterpret_cast<const floatx4*>(mzw_opaque(L.s)) + lane;
   const float* B1 = L.b1 + 4 * g;
 #pragma unroll
   for (int ot = 0; ot < NO; ++ot)
