@@ -117,7 +117,8 @@ extern "C" int mzh_create(int device, int n_disks, int max_sims, int max_roots, 
   eng->kin = ((eng->in_dim + 15) / 16) * 16;
   eng->E = max_sims + 1;
   const size_t nblk = (size_t)max_roots * eng->E;
-  hipError_t e = hipMalloc(&eng->tree, nblk * 128)  /* MzhBlock: one cache line */;
+  // MzhBlock: one cache line per node (MZW_QC builds: two, see mzh_wave.hip MzwNodeQ)
+  hipError_t e = hipMalloc(&eng->tree, nblk * (MZW_QC ? 256 : 128));
   if (e == hipSuccess) e = hipMalloc(&eng->htree, nblk * MZH_LATENT * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&eng->pathx, nblk * sizeof(uint16_t));
   if (e == hipSuccess) e = hipMalloc(&eng->table, sizeof(double) * (size_t)(max_sims + 2));

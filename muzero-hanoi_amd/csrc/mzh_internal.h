@@ -6,6 +6,12 @@
 
 #include "mzh_device.h"
 
+#include <type_traits>
+
+#ifndef MZW_QC
+#define MZW_QC 0  // wave kernel: cached child values in the tree block (mzh_wave.hip)
+#endif
+
 struct MzhSearchParams {
   int B, S, E;          // roots, simulations, tree blocks per root (engine max_sims + 1)
   int in_dim, kin;      // observation width 3N and its zero-padded width (16 * rep0.kb)

@@ -75,6 +75,9 @@
                       // loop-invariant weight fragments are not hoisted out of the simulation loop (which
                       // kept them live in VGPRs through the tree phases: 256 VGPRs + spills without it)
 #endif
+// MZW_QC (default 0, mzh_internal.h): cache each child's value R + disc * W / N (fp64, written by
+// backup) in the tree block in place of W, so selection skips that division; W moves to the node's
+// second cache line (256-B nodes) and reaches backup through the LDS snapshot
 #ifndef MZW_FENCE
 #define MZW_FENCE 1   // 1: workgroup-scope fence at the end of each simulation, 0: wavefront scope
 #endif
@@ -92,11 +95,26 @@ struct __align__(128) MzwBlock {
   uint32_t pad[2];
 };
 static_assert(sizeof(MzwBlock) == 128, "block layout");
+// MZW_QC: node = the select line (MzwBlock, W[] holding the cached child values) + a line with W
+struct __align__(128) MzwNodeQ {
+  MzwBlock b;
+  double W[6];
+  uint32_t pad[20];
+};
+static_assert(sizeof(MzwNodeQ) == 256, "node layout");
+using MzwNode = std::conditional<MZW_QC != 0, MzwNodeQ, MzwBlock>::type;
+__device__ __forceinline__ MzwBlock& mzw_blk(MzwBlock* t, int e) { return t[e]; }
+__device__ __forceinline__ MzwBlock& mzw_blk(MzwNodeQ* t, int e) { return t[e].b; }
+__device__ __forceinline__ double& mzw_wref(MzwBlock* t, int e, int a) { return t[e].W[a]; }
+__device__ __forceinline__ double& mzw_wref(MzwNodeQ* t, int e, int a) { return t[e].W[a]; }
 
 // per-wave LDS: the roots' own children (SoA, lane = root: conflict-free) and the path cache
 template <int ROOTS>
 struct MzwWave {
   double rW[6][ROOTS];
+#if MZW_QC
+  double rQ[6][ROOTS];  // cached child values of the root's children
+#endif
   double rP[6][ROOTS];  // fp64 prior (Dirichlet-mixed or the widened fp32 prior)
   float rR[6][ROOTS];
   int rN[6][ROOTS];
@@ -516,6 +534,15 @@ __device__ __forceinline__ float mzw_ucb(int Nc, double Wc, float Rc, double P64
   const float u32 = p64_semantics ? (float)(P64 * w) : (float)P64 * (float)w;
   return q32 + u32;
 }
+// the same UCB from a cached child value v = R + disc * W / N (MZW_QC)
+__device__ __forceinline__ float mzw_ucbq(int Nc, double v, double P64, bool p64_semantics, double tnp, bool has,
+                                          double mn, double den, double dinv, const double* inv) {
+  float q32 = 0.0f;
+  if (Nc > 0) q32 = (float)(has ? mzw_div(v - mn, den, dinv) : v);
+  const double w = mzw_div(tnp, (double)(Nc + 1), mzw_rcp(Nc + 1, inv));
+  const float u32 = p64_semantics ? (float)(P64 * w) : (float)P64 * (float)w;
+  return q32 + u32;
+}
 // in-lane argmax over 6 children with the reference's tie handling (see mzh_group_pick)
 __device__ __forceinline__ int mzw_pick(const float (&u)[6], int tie, int& firstTie, int& extra) {
   float m = u[0];
@@ -566,7 +593,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
   const int rho = lane;
   const int rroot = wr0 + rho;
   const bool rvalid = lane < ROOTS && rroot < p.B;
-  MzwBlock* tb = reinterpret_cast<MzwBlock*>(p.tree) + (size_t)(rvalid ? rroot : 0) * E;
+  MzwNode* tb = reinterpret_cast<MzwNode*>(p.tree) + (size_t)(rvalid ? rroot : 0) * E;
   double mmax = -__builtin_inf(), mmin = __builtin_inf();
   if (rvalid && p.minmax_in) {
     mmax = p.minmax_in[2 * rroot];
@@ -649,6 +676,9 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
 #pragma unroll
     for (int c = 0; c < MZH_A; ++c) {
       ws.rW[c][rho] = 0.0;
+#if MZW_QC
+      ws.rQ[c][rho] = 0.0;
+#endif
       ws.rR[c][rho] = 0.0f;
       ws.rN[c][rho] = 0;
       ws.rX[c][rho] = -1;
@@ -665,6 +695,15 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
   float val[NT], rew[NT];
   floatx4 cpi[NT];
 
+  auto mzw_rq = [&](int c) -> double {  // cached value of root child c (MZW_QC)
+#if MZW_QC
+    return ws.rQ[c][rho];
+#else
+    (void)c;
+    return 0.0;
+#endif
+  };
+
   // T-phase part 1: select one leaf per root, then gather its parent latent
   auto phase_select = [&](int s) {
     if (MZW_ONLYM) {  // DIAGNOSTIC ONLY: no tree work (the MLP always expands the root's first child)
@@ -678,8 +717,10 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
       const double tr = table[rootN];
 #pragma unroll
       for (int c = 0; c < MZH_A; ++c)
-        u[c] = mzw_ucb(ws.rN[c][rho], ws.rW[c][rho], ws.rR[c][rho], ws.rP[c][rho], noised || p.np1, tr, disc, has,
-                       mmin, den, dinv, inv);
+        u[c] = MZW_QC ? mzw_ucbq(ws.rN[c][rho], mzw_rq(c), ws.rP[c][rho], noised || p.np1, tr, has, mmin, den,
+                                 dinv, inv)
+                      : mzw_ucb(ws.rN[c][rho], ws.rW[c][rho], ws.rR[c][rho], ws.rP[c][rho], noised || p.np1, tr, disc,
+                                has, mmin, den, dinv, inv);
       int pick = mzw_pick(u, tie, firstTie, extra);
       int Np = ws.rN[pick][rho], X = ws.rX[pick][rho];
       ws.path[0][rho] = (uint16_t)pick;
@@ -696,9 +737,11 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
           pf[c] = *reinterpret_cast<const int*>(tb + (xc >= 0 ? xc : 0));
         }
       }
+      double wpend = 0.0;  // MZW_QC: the chosen child's W (second node line), in flight to pcW[dpend]
+      int dpend = -1;
       while (X >= 0 && d <= S) {  // depth <= s + 1 always; the bound only guards against a corrupt tree
         e = X;
-        const int4* bp = reinterpret_cast<const int4*>(tb + e);
+        const int4* bp = reinterpret_cast<const int4*>(&mzw_blk(tb, e));
         int dw[32];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -724,9 +767,15 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
 #pragma unroll
         for (int c = 0; c < MZH_A; ++c) {
           Rc[c] = __int_as_float(dw[6 + c]);
-          Wc[c] = __hiloint2double(dw[19 + 2 * c], dw[18 + 2 * c]);
-          u[c] = mzw_ucb(dw[c] & 0xFFFF, Wc[c], Rc[c], (double)__int_as_float(dw[12 + c]), p.np1, table[Np], disc,
-                         has, mmin, den, dinv, inv);
+          Wc[c] = __hiloint2double(dw[19 + 2 * c], dw[18 + 2 * c]);  // MZW_QC: the cached child value
+          u[c] = MZW_QC ? mzw_ucbq(dw[c] & 0xFFFF, Wc[c], (double)__int_as_float(dw[12 + c]), p.np1, table[Np], has,
+                                   mmin, den, dinv, inv)
+                        : mzw_ucb(dw[c] & 0xFFFF, Wc[c], Rc[c], (double)__int_as_float(dw[12 + c]), p.np1, table[Np],
+                                  disc, has, mmin, den, dinv, inv);
+        }
+        if (MZW_QC && dpend >= 0) {  // the previous level's W load is older than this block's loads
+          ws.pcW[dpend][rho] = wpend;
+          dpend = -1;
         }
         pick = mzw_pick(u, tie, firstTie, extra);
         int nx = dw[0];
@@ -744,7 +793,12 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
         const uint16_t slot = (uint16_t)(e * 8 + pick);
         if (d < MZW_DC) {
           ws.path[d][rho] = slot;
-          ws.pcW[d][rho] = Wp;
+          if (MZW_QC) {
+            wpend = mzw_wref(tb, e, pick);
+            dpend = d;
+          } else {
+            ws.pcW[d][rho] = Wp;
+          }
           ws.pcR[d][rho] = Rp;
           ws.pcN[d][rho] = Np;
         } else {
@@ -756,6 +810,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
 #pragma unroll
         for (int c = 0; c < MZH_A; ++c) asm volatile("" ::"v"(pf[c]));
       }
+      if (MZW_QC && dpend >= 0) ws.pcW[dpend][rho] = wpend;
       depth = d;
       leafE = e;
       leafA = pick;
@@ -836,7 +891,8 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
           if (!cvalid[n]) continue;
-          MzwBlock* nb = reinterpret_cast<MzwBlock*>(p.tree) + (size_t)croot[n] * E + (s + 1);
+          MzwNode* nn = reinterpret_cast<MzwNode*>(p.tree) + (size_t)croot[n] * E;
+          MzwBlock* nb = &mzw_blk(nn, s + 1);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int c = 4 * g + i;
@@ -845,6 +901,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
               nb->R[c] = 0.0f;
               nb->P[c] = cpi[n][i];
               nb->W[c] = 0.0;
+              if (MZW_QC) mzw_wref(nn, s + 1, c) = 0.0;
             }
           }
         }
@@ -857,13 +914,14 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
       if (REPLAY) {
         vv = p.rp_value[(size_t)rroot * S + s];
         rr = p.rp_reward[(size_t)rroot * S + s];
-        MzwBlock* nb = tb + enew;
+        MzwBlock* nb = &mzw_blk(tb, enew);
 #pragma unroll
         for (int c = 0; c < MZH_A; ++c) {
           *reinterpret_cast<uint32_t*>(&nb->nx[c]) = 0xFFFF0000u;
           nb->R[c] = 0.0f;
           nb->P[c] = p.rp_pi[((size_t)rroot * S + s) * MZH_A + c];
           nb->W[c] = 0.0;
+          if (MZW_QC) mzw_wref(tb, enew, c) = 0.0;
         }
       } else {
         // root lane rho is column rho & 15 of tile rho >> 4 (every row of a column holds its scalars)
@@ -880,8 +938,8 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
         ws.rX[leafA][rho] = enew;
         ws.rR[leafA][rho] = rr;
       } else {
-        tb[leafE].nx[leafA].X = (int16_t)enew;
-        tb[leafE].R[leafA] = rr;
+        mzw_blk(tb, leafE).nx[leafA].X = (int16_t)enew;
+        mzw_blk(tb, leafE).R[leafA] = rr;
       }
       double v = (double)vv;
       double lmax = -__builtin_inf(), lmin = __builtin_inf();
@@ -896,9 +954,9 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
         } else {
           slot = p.pathx[(size_t)rroot * E + j];
           const int e = slot >> 3, a = slot & 7;
-          W = tb[e].W[a];
-          R = tb[e].R[a];
-          N = tb[e].nx[a].N;
+          W = mzw_wref(tb, e, a);
+          R = mzw_blk(tb, e).R[a];
+          N = mzw_blk(tb, e).nx[a].N;
         }
       };
       int slot;
@@ -916,14 +974,20 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 8 / MZW_WAVES) void mzh_wave_kernel
         const double rw = (j == depth - 1) ? (double)rr : (double)Rj;
         const double Wn = Wj + v;
         const int Nn = Nj + 1;
+        // the child's value after this backup: MinMaxStats input, and (MZW_QC) the cached value its
+        // next selection reads -- the same operations as mzw_ucb's v
+        const double q = rw + disc * mzw_div(Wn, (double)Nn, mzw_rcp(Nn, inv));
         if (e == 0) {
           ws.rW[a][rho] = Wn;
           ws.rN[a][rho] = Nn;
+#if MZW_QC
+          ws.rQ[a][rho] = q;
+#endif
         } else {
-          tb[e].W[a] = Wn;
-          tb[e].nx[a].N = (uint16_t)Nn;
+          mzw_wref(tb, e, a) = Wn;
+          mzw_blk(tb, e).nx[a].N = (uint16_t)Nn;
+          if (MZW_QC) mzw_blk(tb, e).W[a] = q;
         }
-        const double q = rw + disc * mzw_div(Wn, (double)Nn, mzw_rcp(Nn, inv));
         lmax = q > lmax ? q : lmax;
         lmin = q < lmin ? q : lmin;
         v = rw + disc * v;
