@@ -4,19 +4,27 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W             # N>1, one rank per GPU
 
-Workload: 4-disk Hanoi, 50 simulations per move, 65,536 random non-goal root states per GPU -- the
-metric's 65k-root batch on every GPU (weak scaling: N GPUs search N independent 65k-root batches;
-BASELINE configs[2], the same batch sharded 8 ways, is `--roots-per-gpu 8192`), MuZeroNet(TD_return=True) with
-random-init weights (torch.manual_seed(0), broadcast once), training-like search parameters
-(gamma 0.8, Dirichlet alpha 0.25 / eps 0.25, T=1, stochastic).  One step = one mzh_search launch
-over every root on the rank (root inference + 50 x {select, MFMA MLP, backup} + play policy),
-followed by the RCCL all_gather of the visit histograms (north_star's only exchange).  Inputs are
-resident in HBM before timing starts.
+Workload (default): BASELINE.json's metric batch, 65,536 random non-goal 4-disk root states x 50
+simulations, sharded contiguously over the N GPUs (strong scaling: 65,536 roots on 1 GPU, 8,192 per
+GPU at N=8 = BASELINE configs[2] exactly).  `--config K` selects BASELINE configs[K] instead
+(1: 4,096 roots S=50; 2: the default; 3: 16,384 roots S=200 N=4; 4: 262,144 roots S=100 N=7, sharded
+over the ranks); `--roots-per-gpu B` runs B roots on every GPU (weak scaling, labelled so).
+MuZeroNet(TD_return=True) with random-init weights (torch.manual_seed(0), broadcast once),
+training-like search parameters (gamma 0.8, Dirichlet alpha 0.25 / eps 0.25, T=1, stochastic).
+One step = one mzh_search launch over every root on the rank (root inference + S x {select, MFMA
+MLP, backup} + play policy), followed by the RCCL all_gather of the visit histograms
+(north_star's only exchange).  Inputs are resident in HBM before timing starts.
 
-Rank 0 prints ONE JSON line (contract in the task statement) including `roofline` for the
-fused search kernel (fp32-MFMA bound; achieved = algorithmic matmul FLOPs per launch / mean
-launch time from HIP events on the launch stream) and `cpu_baseline` (the reference algorithm's
-Python restatement, oracle/py_port.py, on one host core over a bounded sample).
+Rank 0 prints ONE JSON line (contract in the task statement) including
+  roofline        the fused search kernel (fp32-MFMA bound; achieved = algorithmic matmul FLOPs per
+                  launch / mean launch time from HIP events on the launch stream);
+  roofline.tree   select / expand / backup (HBM-bound): the same kernel's replay instantiation --
+                  identical tree code with the network outputs read from HBM instead of computed --
+                  timed live on the same roots; algorithmic tree bytes from the
+                  kernel's own selection-step counts / its HIP-event time;
+  cpu_baseline    the reference algorithm's Python restatement (oracle/py_port.py: object tree,
+                  batch-1 torch-CPU MLP, NumPy RNG) as one process per host core over a bounded
+                  sample (N=1 only), run before the GPU is touched.
 """
 import argparse
 import json
@@ -31,7 +39,22 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (matrix), spec
+HBM_PEAK_GBPS = 8000.0         # MI355X_MICROARCH.md: HBM3E peak (spec)
 MLP_FLOP_PER_SIM = 203_776     # recurrent_inference matmul FLOPs (2 x 101,888 MAC)
+# SURVEY.md 8d tree bytes: 124 B per selection step, 28 B per backed-up path node, 540 B per expansion
+SEL_BYTES, BACKUP_BYTES, EXPAND_BYTES = 124, 28, 540
+# the replay instantiation expands from recorded outputs: 32 B read (6 priors, value, reward) and the
+# new child statistics written (6 priors + the leaf reward = 28 B); no latent is read or written
+EXPAND_BYTES_REPLAY = 32 + 28
+
+METRIC = "MCTS sims/sec (node) 4-disk Hanoi, 50 sims/move, 65k root batch; 1/2/4/8 GPU"
+# BASELINE.json configs[1..4]: (disks, global roots, sims, description)
+CONFIGS = {
+    1: (4, 4096, 50, "BASELINE configs[1]: 4-disk, 4,096-root batch, 50 sims/move"),
+    2: (4, 65536, 50, "BASELINE configs[2]: 4-disk, 65,536 roots, 50 sims/move, sharded over the GPUs"),
+    3: (4, 16384, 200, "BASELINE configs[3]: 4-disk, 16,384 roots, 200 sims/move (deep tree)"),
+    4: (7, 262144, 100, "BASELINE configs[4]: 7-disk, 262,144 roots, 100 sims/move, sharded over the GPUs"),
+}
 
 
 def root_flops(n_disks):
@@ -43,15 +66,21 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--roots-per-gpu", type=int, default=65536)
-    p.add_argument("--sims", type=int, default=50)
-    p.add_argument("--disks", type=int, default=4)
+    p.add_argument("--config", type=int, choices=sorted(CONFIGS), default=2,
+                   help="BASELINE.json configs[K]; the global batch is sharded over the ranks (strong scaling)")
+    p.add_argument("--roots-per-gpu", type=int, default=None,
+                   help="weak scaling: this many roots on every GPU (overrides the config's global batch)")
+    p.add_argument("--sims", type=int, default=None)
+    p.add_argument("--disks", type=int, default=None)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-gather", action="store_true")
+    p.add_argument("--no-tree", action="store_true", help="skip the live select/backup (replay) measurement")
     p.add_argument("--kernel", choices=["auto", "coop", "wave", "wave16"], default="auto")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, one rank per GPU); gloo lets ranks share a GPU to rehearse the N>1 path")
     p.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    p.add_argument("--cpu-baseline-procs", type=int, default=0,
+                   help="0: one process per available host core (capped at 16, the GPU box's CPU share)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return p.parse_args()
@@ -68,28 +97,65 @@ def random_roots(n_disks, B, seed):
     return obs
 
 
-def cpu_baseline(n_disks, S, seconds, seed):
-    """oracle/py_port.py (object tree, batch-1 torch-CPU MLP, NumPy RNG) on one core."""
+# ------------------------------------------------------------------------------------------------
+# CPU baseline: the reference algorithm (oracle/py_port.py restates MCTS/mcts.py:34-126 + node.py +
+# networks.py and matches the reference's visit counts bit for bit) on the host cores.
+# ------------------------------------------------------------------------------------------------
+def _cpu_worker(args):
+    """one host process: fresh MCTS per root over roots k, k + P, k + 2P, ... for `seconds`"""
+    n_disks, S, seconds, seed, k, P = args
+    torch.set_num_threads(1)
     from muzero_hanoi_amd.networks import MuZeroNet
     from oracle import py_port
 
-    torch.set_num_threads(1)
     torch.manual_seed(seed)
     net = MuZeroNet(3 * n_disks, 6, 0.002, "cpu", TD_return=True)
-    pnet = py_port.PortNet({k: v.numpy() for k, v in net.state_dict().items()})
+    pnet = py_port.PortNet({kk: v.numpy() for kk, v in net.state_dict().items()})
     obs = random_roots(n_disks, 4096, seed + 99).astype(np.float64)
-    np.random.seed(seed)
+    np.random.seed(seed + k)
     roots = 0
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds and roots < len(obs):
+    r = k
+    while time.perf_counter() - t0 < seconds:
         m = py_port.PortMCTS(0.8, 0.25, S)
-        m.run_mcts(obs[roots], pnet, 1.0, False)
+        m.run_mcts(obs[r % len(obs)], pnet, 1.0, False)
         roots += 1
-    dt = time.perf_counter() - t0
-    return {"value": roots * S / dt, "unit": "sims/s", "cores": 1, "kind": "port",
-            "sample": f"{roots} roots x {S} sims, {n_disks}-disk, fresh MCTS per root, T=1 stochastic, "
-                      f"{dt:.1f} s on 1 host core (torch threads=1); oracle/py_port.py restates "
-                      f"MCTS/mcts.py + networks.py and matches the reference's visits bit-exactly"}
+        r += P
+    return roots, time.perf_counter() - t0
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(n_disks, S, seconds, seed, procs=0):
+    """One process per host core (torch.set_num_threads(1) each, roots partitioned round-robin),
+    aggregate sims/s = all processes' sims / the slowest process's wall time; plus the 1-process
+    figure from a separate single-process run of the same length."""
+    import multiprocessing as mp
+
+    avail = len(os.sched_getaffinity(0))
+    P = procs if procs > 0 else min(avail, 16)
+    ctx = mp.get_context("spawn")  # fresh interpreters; this process has not touched the GPU
+    single_roots, single_dt = _cpu_worker((n_disks, S, seconds / 3, seed, 0, 1))
+    with ctx.Pool(P) as pool:
+        res = pool.map(_cpu_worker, [(n_disks, S, seconds, seed, k, P) for k in range(P)])
+    roots = sum(r for r, _ in res)
+    dt = max(t for _, t in res)
+    return {"value": roots * S / dt, "unit": "sims/s", "cores": P, "kind": "port",
+            "cpu_model": _cpu_model(), "cores_available": avail,
+            "single_core_value": single_roots * S / single_dt,
+            "sample": f"{P} processes x {seconds:.0f} s (one per host core, torch threads=1 each): {roots} roots x "
+                      f"{S} sims, {n_disks}-disk, fresh MCTS per root, T=1 stochastic, roots partitioned "
+                      f"round-robin; single_core_value: 1 process, {single_roots} roots in {single_dt:.1f} s. "
+                      f"oracle/py_port.py restates MCTS/mcts.py + networks.py and matches the reference's "
+                      f"visits bit-exactly"}
 
 
 def cpu_baseline_selfplay(n_disks, S, max_steps, seconds, net_state, start_state):
@@ -132,6 +198,19 @@ def cpu_baseline_solver(states, seconds):
     return np.array(ref, np.int32), k / (time.perf_counter() - t0)
 
 
+def tree_bytes(sel_steps_sum, n_roots, S, expand_bytes):
+    """SURVEY.md 8d algorithmic tree bytes: 124 per selection step, 28 per backed-up node (each
+    simulation backs up its d selected path nodes + the root), expand_bytes per expansion"""
+    return SEL_BYTES * sel_steps_sum + BACKUP_BYTES * (sel_steps_sum + n_roots * S) + expand_bytes * n_roots * S
+
+
+def kernel_name(kern, B):
+    kern_sel = kern if kern != "auto" else ("wave" if B >= 53248 else "wave16" if B > 8192 else "coop")
+    coop_rows = 32 if B > 4096 else 16  # mzh_api.hip choose_kernel() / pick_rows()
+    return kern_sel, {"wave": "mzh_wave_kernel<2,{r},true>", "wave16": "mzh_wave_kernel<1,{r},true>",
+                      "coop": f"mzh_search_kernel<{coop_rows},{{r}},*>"}[kern_sel]
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -139,6 +218,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world and world > 1:
         raise SystemExit(f"--gpus {a.gpus} != WORLD_SIZE {world}")
+    N, GB, S, desc = CONFIGS[a.config]
+    N = a.disks or N
+    S = a.sims or S
+    weak = a.roots_per_gpu is not None
+    if weak:
+        GB = world * a.roots_per_gpu
+
+    # CPU baseline first (rank 0, N=1): spawned host processes, before this process touches the GPU
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(N, S, a.cpu_baseline_seconds, a.seed, a.cpu_baseline_procs)
+
     ndev = torch.cuda.device_count()
     if a.dist_backend == "nccl" and world > 1 and local >= ndev:
         raise SystemExit(f"LOCAL_RANK {local} but only {ndev} GPUs (RCCL needs one GPU per rank)")
@@ -158,8 +249,8 @@ def main():
     from muzero_hanoi_amd import engine, rng
     from muzero_hanoi_amd.networks import MuZeroNet
 
-    N, S, B = a.disks, a.sims, a.roots_per_gpu
-    GB = world * B  # global roots (weak scaling)
+    s0, s1 = mdist.shard_range(GB, world, rank)
+    B = s1 - s0  # this rank's roots
     torch.manual_seed(a.seed)
     net = MuZeroNet(3 * N, 6, 0.002, "cpu", TD_return=True)
     flat = engine.flat_weights(net.state_dict())
@@ -178,19 +269,19 @@ def main():
     kern = None if a.kernel == "auto" else a.kernel
     stream = torch.cuda.current_stream(dev)
 
-    def step():
+    def search():
         eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, temperature=1.0, deterministic=False,
                    discount=0.8, eps=0.25, out=out, kernel=kern)
-        if gather:
-            return mdist.gather_visits(out["visits"], GB, world)
 
     for _ in range(a.warmup):
-        step()
+        search()
+        if gather:
+            mdist.gather_visits(out["visits"], GB, world)
     torch.cuda.synchronize(dev)
     # correctness sanity on the warmed-up result (outside timing)
     vis = out["visits"]
     assert int(vis.sum(1).min()) == S and int(vis.sum(1).max()) == S, "visit counts do not sum to n_sims"
-    sel_mean = float(out["sel_steps"].double().mean()) / S
+    sel_sum = float(out["sel_steps"].double().sum())
 
     # kernel-time probe: HIP events on the launch stream around each search launch
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
@@ -200,8 +291,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(a.steps):
         evs[k][0].record(stream)
-        eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, temperature=1.0, deterministic=False,
-                   discount=0.8, eps=0.25, out=out, kernel=kern)
+        search()
         evs[k][1].record(stream)
         if gather:
             mdist.gather_visits(out["visits"], GB, world)
@@ -210,30 +300,77 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+
+    # select / expand / backup alone: the replay instantiation of the same kernel on the same roots,
+    # network outputs drawn like a random-init network's (near-uniform priors, small values)
+    tree = None
+    if not a.no_tree:
+        g = np.random.default_rng(a.seed + 7)
+        rp = dict(root_pi=torch.from_numpy(g.dirichlet(np.full(6, 20.0), size=B).astype(np.float32)).to(dev),
+                  pi=torch.from_numpy(g.dirichlet(np.full(6, 20.0), size=(B, S)).astype(np.float32)).to(dev),
+                  reward=torch.from_numpy(g.normal(0, 0.05, (B, S)).astype(np.float32)).to(dev),
+                  value=torch.from_numpy(g.normal(0, 0.5, (B, S)).astype(np.float32)).to(dev))
+        rout = eng.alloc_search_outputs(B, S)
+
+        def replay():
+            eng.search(S, replay=rp, tie_idx=tie, noise=noise, action_u=u, temperature=1.0, deterministic=False,
+                       discount=0.8, eps=0.25, out=rout, kernel=kern)
+
+        replay()
+        torch.cuda.synchronize(dev)
+        rsel = float(rout["sel_steps"].double().sum())
+        tev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+        for s_, e_ in tev:
+            s_.record(stream)
+            replay()
+            e_.record(stream)
+        torch.cuda.synchronize(dev)
+        tree_ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in tev]))
+        tb = tree_bytes(rsel, B, S, EXPAND_BYTES_REPLAY)
+        tree = {"bound": "hbm", "kernel": kernel_name(a.kernel, B)[1].format(r="true"),
+                "bytes_per_launch": tb, "kernel_ms": tree_ms, "achieved": tb / (tree_ms * 1e-3) / 1e9,
+                "peak": HBM_PEAK_GBPS, "unit": "GB/s", "sel_steps_per_sim": rsel / (B * S),
+                "frac": tb / (tree_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "traffic": None,
+                "fused_tree_bytes_per_launch": tree_bytes(sel_sum, B, S, EXPAND_BYTES),
+                "what": "select/expand/backup only: the search kernel's replay instantiation (same tree code, "
+                        "network outputs read from HBM), same roots and draws; bytes = SURVEY.md 8d (124 B per "
+                        "selection step, 28 B per backed-up node, 60 B per replayed expansion) with the kernel's "
+                        "own selection-step count; fused_tree_bytes_per_launch: the same count in the fused "
+                        "search (540 B per expansion incl. the latent read/write)"}
+
     if dist is not None:
-        t = torch.tensor([dt, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt, kern_ms, tree["kernel_ms"] if tree else 0.0], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, kern_ms = float(t[0]), float(t[1])
+        if tree:
+            tree["kernel_ms"] = float(t[2])
+            tree["achieved"] = tree["bytes_per_launch"] / (tree["kernel_ms"] * 1e-3) / 1e9
+            tree["frac"] = tree["achieved"] / HBM_PEAK_GBPS
 
-    sims_total = world * B * S * a.steps
+    sims_total = GB * S * a.steps
     value = sims_total / dt
     flops_launch = B * (S * MLP_FLOP_PER_SIM + root_flops(N))
     achieved = flops_launch / (kern_ms * 1e-3) / 1e12
-    kern_sel = a.kernel if a.kernel != "auto" else ("wave" if B >= 53248 else "wave16" if B > 8192 else "coop")
-    coop_rows = 32 if B > 4096 else 16  # mzh_api.hip choose_kernel() / pick_rows()
-    kernel_name = {"wave": "mzh_wave_kernel<2,false,true>", "wave16": "mzh_wave_kernel<1,false,true>",
-                   "coop": f"mzh_search_kernel<{coop_rows},false,*>"}[kern_sel]
+    kname = kernel_name(a.kernel, B)[1].format(r="false")
     traffic = None
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
             if tj.get("workload") == f"hanoi{N}_s{S}_roots{B}":
                 traffic = tj.get("hbm_bytes_per_launch")
+                if tree is not None:
+                    tree["traffic"] = tj.get("tree_hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
+    if weak:
+        workload = (f"weak scaling: {N}-disk, {B} roots per GPU ({GB} over {world} GPUs), {S} sims/move "
+                    f"(not a BASELINE config unless N x roots matches one)")
+    else:
+        workload = desc + (f": {B} roots per GPU at N={world}" if world > 1 else
+                           (" (the whole batch on one GPU)" if a.config in (2, 4) else ""))
     result = {
-        "metric": "MCTS sims/sec (node) 4-disk Hanoi, 50 sims/move, 65k root batch; 1/2/4/8 GPU",
+        "metric": METRIC,
         "value": value,
         "unit": "sims/s",
         "n_gpus": world,
@@ -241,22 +378,19 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": dt / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if weak else "strong",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic: uniform random non-goal 4-disk root states, random-init MuZeroNet(TD_return=True)",
-        "config": {"workload": f"hanoi{N}_s{S}_roots{B}_per_gpu" + (" (the metric's 65k-root batch on every GPU, weak scaling)"
-                                                                   if B == 65536 else " (weak scaling)"),
-                   "n_disks": N, "sims_per_move": S, "roots_per_gpu": B, "global_roots": world * B,
+        "data": f"synthetic: uniform random non-goal {N}-disk root states, random-init MuZeroNet(TD_return=True)",
+        "config": {"workload": workload, "baseline_config": None if weak else a.config, "n_disks": N,
+                   "sims_per_move": S, "roots_per_gpu": B, "global_roots": GB,
                    "parallelism": f"dp{world} (independent roots, all_gather of visits)" if world > 1 else "dp1"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": kernel_name, "kernel_ms": kern_ms,
-                     "flop_per_launch": flops_launch, "sel_steps_per_sim": sel_mean},
-        "cpu_baseline": None,
+                     "kernel": kname, "kernel_ms": kern_ms,
+                     "flop_per_launch": flops_launch, "sel_steps_per_sim": sel_sum / (B * S), "tree": tree},
+        "cpu_baseline": cpu,
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(N, S, a.cpu_baseline_seconds, a.seed)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:

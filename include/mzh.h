@@ -203,16 +203,6 @@ int mzh_train_scratch_bytes(int B, int U, int in_dim, int support, size_t* bytes
 int mzh_train_transpose(const mzh_train_args* args, mzh_stream stream);
 int mzh_train_update(const mzh_train_args* args, mzh_stream stream);
 
-/* ---------------------------------------------------------------------------------------------
- * Device self-tests of numerical building blocks the kernels rely on (no reference equivalent;
- * used by tests/test_gpu_parity.py).  Adds the number of failures to *result (device int32).
- *   MZH_SELFTEST_RCP: the search kernels' register reciprocal RN(1/n) equals IEEE 1.0 / n for
- *                     every integer n in [1, n] (the Markstein divisions of node.py's W/N and
- *                     w/(N+1) need it exact).
- * ------------------------------------------------------------------------------------------- */
-#define MZH_SELFTEST_RCP 1
-int mzh_selftest(int test, int n, int32_t* result, mzh_stream stream);
-
 #ifdef __cplusplus
 }
 #endif

@@ -23,7 +23,6 @@ MZH_FLAG_NP1_UCB = 1
 MZH_FLAG_KERNEL_COOP = 2  # cooperative kernel (mzh_search.hip)
 MZH_FLAG_KERNEL_WAVE = 4  # wave-independent kernel (mzh_wave.hip), 32 roots per wave
 MZH_FLAG_KERNEL_WAVE16 = 8  # wave-independent kernel, 16 roots per wave
-MZH_SELFTEST_RCP = 1
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -71,7 +70,6 @@ SIGNATURES = {
     "mzh_recurrent_inference": (ctypes.c_int, [_vp, ctypes.c_int] + [_vp] * 9 + [_vp]),
     "mzh_search": (ctypes.c_int, [_vp, ctypes.POINTER(SearchArgs), _vp]),
     "mzh_search_replay": (ctypes.c_int, [_vp, ctypes.POINTER(SearchArgs), _vp]),
-    "mzh_selftest": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _vp]),
     "mzh_train_scratch_bytes": (ctypes.c_int, [ctypes.c_int] * 4 + [ctypes.POINTER(ctypes.c_size_t)]),
     "mzh_train_transpose": (ctypes.c_int, [ctypes.POINTER(TrainArgs), _vp]),
     "mzh_train_update": (ctypes.c_int, [ctypes.POINTER(TrainArgs), _vp]),

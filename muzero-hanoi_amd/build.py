@@ -37,6 +37,12 @@ def build(verbose=False, force=False, diag=False, tag="", defines=()):
     lib_path = LIB.replace("libmzh.so", f"libmzh{sfx}.so")
     flags = FLAGS + (["-DMZH_STAMPS"] if diag else []) + [f"-D{d}" for d in defines]
     os.makedirs(obj_dir, exist_ok=True)
+    # the objects of a variant directory are only reusable for the same flags: a stamp file records
+    # them, and a change forces a rebuild (A/B builds of one tag with different -D lists)
+    stamp = os.path.join(obj_dir, "flags.txt")
+    want = " ".join(flags)
+    if not os.path.exists(stamp) or open(stamp).read() != want:
+        force = True
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     headers.append(os.path.join(REPO, "include", "mzh.h"))
     jobs = []
@@ -62,6 +68,10 @@ def build(verbose=False, force=False, diag=False, tag="", defines=()):
     if force or jobs or _stale(lib_path, objs):
         run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", lib_path,
              "-Wl,-rpath,/opt/rocm/lib"])
+    with open(stamp, "w") as f:
+        f.write(want)
+    with open(lib_path + ".flags", "w") as f:  # what this .so was built with (A/B logs cite it)
+        f.write(want + "\n")
     return lib_path
 
 

@@ -118,7 +118,7 @@ extern "C" int mzh_create(int device, int n_disks, int max_sims, int max_roots, 
   eng->E = max_sims + 1;
   const size_t nblk = (size_t)max_roots * eng->E;
   // MzhBlock: one cache line per node (MZW_QC builds: two, see mzh_wave.hip MzwNodeQ)
-  hipError_t e = hipMalloc(&eng->tree, nblk * (MZW_QC ? 256 : 128));
+  hipError_t e = hipMalloc(&eng->tree, nblk * 128);  // one 128-B block per expanded node
   if (e == hipSuccess) e = hipMalloc(&eng->htree, nblk * MZH_LATENT * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&eng->pathx, nblk * sizeof(uint16_t));
   if (e == hipSuccess) e = hipMalloc(&eng->table, sizeof(double) * (size_t)(max_sims + 2));
@@ -479,13 +479,6 @@ static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream s
 
 extern "C" int mzh_search(mzh_engine* eng, const mzh_search_args* args, mzh_stream stream) {
   return search_common(eng, args, stream, false);
-}
-
-extern "C" int mzh_selftest(int test, int n, int32_t* result, mzh_stream stream) {
-  if (test != MZH_SELFTEST_RCP) return fail(MZH_ERR_ARG, "selftest: unknown test %d", test);
-  if (n < 1 || n > (1 << 24) || !result) return fail(MZH_ERR_ARG, "selftest: bad n=%d / result", n);
-  hipError_t e = mzh_launch_rcp_check(n, result, (hipStream_t)stream);
-  return e == hipSuccess ? MZH_OK : hip_fail(e, "selftest launch");
 }
 
 extern "C" int mzh_search_replay(mzh_engine* eng, const mzh_search_args* args, mzh_stream stream) {

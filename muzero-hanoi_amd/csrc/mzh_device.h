@@ -16,11 +16,9 @@
 #define MZH_H 64
 #define MZH_F 256
 #define MZH_WAVE 64
-// waves per cooperative workgroup: 4, or 8 (two per SIMD, the MLP tiles split eight ways; measured
-// +3% at 6-8k roots with 32-row tiles, -14% at <= 4k roots with 16-row tiles, which then spill)
-#ifndef MZH_WAVES
+// waves per cooperative workgroup (an 8-wave schedule, two per SIMD, measured +3% at 6-8k roots with
+// 32-row tiles and -14% at <= 4k roots with 16-row tiles: not kept)
 #define MZH_WAVES 4
-#endif
 #define MZH_THREADS (64 * MZH_WAVES)
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -603,146 +601,42 @@ __device__ __forceinline__ MzhChunk mzh_pred_tiles(MlpSmem<R>& sm, const MzhNet&
   return c;
 }
 
-// initial_inference (networks.py:71-94): sm.x holds obs rows zero-padded to 16*rep0.kb.  The
-// 4-wave schedule; with 8 waves, waves 4-7 only take part in the barriers (once per search).
+// initial_inference (networks.py:71-94): sm.x holds obs rows zero-padded to 16*rep0.kb
 template <int R>
 __device__ void mzh_mlp_initial(MlpSmem<R>& sm, const MzhNet& net, int wave_in, int lane) {
   constexpr int MT = R / 16;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(wave_in);
-  const bool act = wave < 4;
   floatx4 fa[16], fb[16];
   float ba[4], bb[4];
-  if (act) {  // rep0: 16 tiles, 4 per wave (K = 3N padded: runtime k-blocks)
+  {  // rep0: 16 tiles, 4 per wave (K = 3N padded: runtime k-blocks)
     MzhJob jobs[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) jobs[q] = mzh_job(sm.x, MZH_LD64, net.rep0, wave * 4 + q, sm.hidP, MZH_LD256, 1);
     mzh_run_jobs<MT, 4>(jobs, net.rep0.kb, nullptr, nullptr, lane);
   }
   __syncthreads();
-  if (act) {  // rep2: 4 tiles, 1 per wave
+  {  // rep2: 4 tiles, 1 per wave
     MzhJob job = mzh_job(sm.hidP, MZH_LD256, net.rep2, wave, sm.hraw, MZH_LD64, 0);
     mzh_run_jobs<MT, 1>(&job, net.rep2.kb, nullptr, nullptr, lane);
   }
-  const MzhChunk c5 = mzh_pred_chunk<R>(sm, net, act ? wave : 0, 0), c6 = mzh_pred_chunk<R>(sm, net, act ? wave : 0, 1);
-  const MzhChunk c7 = mzh_head_chunk<R>(sm, net, act ? wave : 0);
-  if (act) {
-    mzh_fetch<4, 4, true>(fa, ba, c5, lane);
-    mzh_fetch<4, 4, true>(fb, bb, c6, lane);
-  }
+  const MzhChunk c5 = mzh_pred_chunk<R>(sm, net, wave, 0), c6 = mzh_pred_chunk<R>(sm, net, wave, 1);
+  const MzhChunk c7 = mzh_head_chunk<R>(sm, net, wave);
+  mzh_fetch<4, 4, true>(fa, ba, c5, lane);
+  mzh_fetch<4, 4, true>(fb, bb, c6, lane);
   __syncthreads();
   mzh_normalize_par<R>(sm.hraw, sm.x, tid);
   __syncthreads();
-  if (act) {
-    mzh_mma_store<MT, 4, 4, true>(fa, ba, c5, sm.x, MZH_LD64, true, nullptr, lane);
-    mzh_fetch<1, 16>(fa, ba, c7, lane);
-    mzh_mma_store<MT, 4, 4, true>(fb, bb, c6, sm.x, MZH_LD64, true, nullptr, lane);
-  }
+  mzh_mma_store<MT, 4, 4, true>(fa, ba, c5, sm.x, MZH_LD64, true, nullptr, lane);
+  mzh_fetch<1, 16>(fa, ba, c7, lane);
+  mzh_mma_store<MT, 4, 4, true>(fb, bb, c6, sm.x, MZH_LD64, true, nullptr, lane);
   __syncthreads();
-  if (act) mzh_mma_store<MT, 1, 16>(fa, ba, c7, c7.out[0] == sm.lpol ? sm.hidP : sm.hidV, MZH_LD256, false, nullptr, lane);
+  mzh_mma_store<MT, 1, 16>(fa, ba, c7, c7.out[0] == sm.lpol ? sm.hidP : sm.hidV, MZH_LD256, false, nullptr, lane);
   __syncthreads();
   mzh_heads_par<R>(sm, sm.hidR, net.support, false, tid);
   __syncthreads();
 }
 
-#if MZH_WAVES == 8
-// recurrent_inference (networks.py:96-138) on 8 waves (two per SIMD).  Chunk schedule per wave w:
-//   A  dyn0 tiles 2w, 2w+1 (+ one-hot, relu) -> hidP          [weights prefetched by fetch12]
-//   A2 waves 0-3: dyn2 tile w (K = 256) -> h'                   [fetched by fetch12]
-//   B  rwd0 tiles 2w, 2w+1 on h' -> hidR; normalise h' -> x
-//   C  waves w < n2 (reward layer-2 tiles): rwd2 tile w + prediction tiles 2w, 2w+1; the others
-//      share the remaining 32 - 2 n2 prediction hidden tiles (K = 64) -> hidP / hidV
-//   D  waves 0-3: pol2 / val2 tile (K = 256) -> logits;  then the heads
-// Every output tile is one wave's k-ordered MFMA chain, exactly as in the 4-wave schedule.
-template <int R>
-__device__ __forceinline__ void mzh_mlp_fetch12(MlpSmem<R>& sm, const MzhNet& net, int wave_in, int lane, floatx4* fa,
-                                                float* ba, floatx4* fb, float* bb) {
-  const int wave = __builtin_amdgcn_readfirstlane(wave_in);
-  mzh_fetch<2, 4, true>(fa, ba, mzh_chunk(net.dyn0, wave * 2, 2, sm.hidP, MZH_LD256), lane);
-  if (wave < 4) mzh_fetch<1, 16, true>(fb, bb, mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64), lane);
-}
-
-template <int R, bool NEXT>
-__device__ __forceinline__ void mzh_mlp_recurrent_body(MlpSmem<R>& sm, const MzhNet& net, int wave_in, int lane,
-                                                       floatx4* fa, float* ba, floatx4* fb, float* bb,
-                                                       const float* onehot) {
-  constexpr int MT = R / 16;
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(wave_in);  // wave-uniform -> chunk descriptors in SGPRs
-  const bool lo = wave < 4;
-  MZH_STAMP_DECL
-  {
-    float oh[2 * MT * 4];
-    const int r = lane & 15, g = lane >> 4;
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          oh[(q * MT + m) * 4 + i] = onehot[sm.act[m * 16 + g * 4 + i] * MZH_F + (wave * 2 + q) * 16 + r];
-    MZH_STAMP(0);
-    mzh_mma_store<MT, 2, 4, true>(fa, ba, mzh_chunk(net.dyn0, wave * 2, 2, sm.hidP, MZH_LD256), sm.x, MZH_LD64, true,
-                                  oh, lane);  // dyn0 + one-hot + bias, relu
-  }
-  MZH_STAMP(1);
-  __syncthreads();
-  mzh_fetch<2, 4, true>(fa, ba, mzh_chunk(net.rwd0, wave * 2, 2, sm.hidR, MZH_LD256), lane);
-  if (lo)
-    mzh_mma_store<MT, 1, 16, true>(fb, bb, mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64), sm.hidP, MZH_LD256, false,
-                                   nullptr, lane);  // dyn2 -> h'
-  // phase C assignment (wave-uniform)
-  const int n2 = net.rwd2.nt;
-  const bool r2 = wave < n2;
-  int p0, pc;
-  if (r2) {
-    p0 = 2 * wave;
-    pc = 2;
-  } else {
-    const int idx = wave - n2, nr = 8 - n2, tot = 32 - 2 * n2, b = tot / nr, x = tot % nr;
-    p0 = 2 * n2 + idx * b + (idx < x ? idx : x);
-    pc = b + (idx < x ? 1 : 0);
-  }
-  const int pc1 = pc < 4 ? pc : 4;
-  if (r2)
-    mzh_fetch<1, 16>(fb, bb, mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP), lane);
-  else
-    mzh_fetch<4, 4>(fb, bb, mzh_pred_tiles<R>(sm, net, p0, pc1), lane);
-  MZH_STAMP(3);
-  __syncthreads();
-  mzh_normalize_par<R>(sm.hraw, sm.x, tid);
-  mzh_mma_store<MT, 2, 4, true>(fa, ba, mzh_chunk(net.rwd0, wave * 2, 2, sm.hidR, MZH_LD256), sm.hraw, MZH_LD64, true,
-                                nullptr, lane);  // rwd0 on h' (networks.py:132)
-  MZH_STAMP(6);
-  __syncthreads();
-  if (r2)
-    mzh_fetch<2, 4>(fa, ba, mzh_pred_tiles<R>(sm, net, p0, 2), lane);
-  else if (pc > 4)
-    mzh_fetch<2, 4>(fa, ba, mzh_pred_tiles<R>(sm, net, p0 + 4, pc - 4), lane);
-  if (r2)
-    mzh_mma_store<MT, 1, 16>(fb, bb, mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP), sm.hidR, MZH_LD256, false,
-                             nullptr, lane);  // rwd2 -> reward logits
-  else
-    mzh_mma_store<MT, 4, 4>(fb, bb, mzh_pred_tiles<R>(sm, net, p0, pc1), sm.x, MZH_LD64, true, nullptr, lane);
-  if (lo) mzh_fetch<1, 16>(fb, bb, mzh_head_chunk<R>(sm, net, wave), lane);
-  if (r2)
-    mzh_mma_store<MT, 2, 4>(fa, ba, mzh_pred_tiles<R>(sm, net, p0, 2), sm.x, MZH_LD64, true, nullptr, lane);
-  else if (pc > 4)
-    mzh_mma_store<MT, 2, 4>(fa, ba, mzh_pred_tiles<R>(sm, net, p0 + 4, pc - 4), sm.x, MZH_LD64, true, nullptr, lane);
-  MZH_STAMP(9);
-  __syncthreads();
-  if (lo)
-    mzh_mma_store<MT, 1, 16>(fb, bb, mzh_head_chunk<R>(sm, net, wave), wave == 0 ? sm.hidP : sm.hidV, MZH_LD256,
-                             false, nullptr, lane);  // pol2 / val2
-  if (NEXT) mzh_mlp_fetch12<R>(sm, net, wave, lane, fa, ba, fb, bb);  // next step's first chunks
-  MZH_STAMP(10);
-  __syncthreads();
-  mzh_heads_par<R>(sm, sm.hidR, net.support, true, tid);
-  MZH_STAMP(11);
-  __syncthreads();
-  MZH_STAMP(12);
-}
-#else
 // recurrent_inference (networks.py:96-138), split so the first two chunks' weights (dyn0, dyn2)
 // can be fetched early -- across the search kernel's tree phase -- into fa/fb:
 //   mzh_mlp_fetch12 : issue the loads of chunk 1 (dyn0) into fa and chunk 2 (dyn2) into fb
@@ -831,7 +725,6 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(MlpSmem<R>& sm, const Mzh
   MZH_STAMP(12);
 }
 
-#endif
 
 template <int R>
 __device__ void mzh_mlp_recurrent(MlpSmem<R>& sm, const MzhNet& net, int wave, int lane) {

@@ -6,12 +6,6 @@
 
 #include "mzh_device.h"
 
-#include <type_traits>
-
-#ifndef MZW_QC
-#define MZW_QC 0  // wave kernel: cached child values in the tree block (mzh_wave.hip)
-#endif
-
 struct MzhSearchParams {
   int B, S, E;          // roots, simulations, tree blocks per root (engine max_sims + 1)
   int in_dim, kin;      // observation width 3N and its zero-padded width (16 * rep0.kb)
@@ -108,7 +102,6 @@ struct MzhWNet {
 };
 
 size_t mzh_wave_smem_bytes(int S, int nt);
-hipError_t mzh_launch_rcp_check(int nmax, int32_t* bad, hipStream_t stream);
 hipError_t mzh_launch_wave_search(int nt, bool replay, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream);
 size_t mzh_search_smem_bytes(int R, int S);
 hipError_t mzh_launch_search(int R, bool replay, const MzhNet& net, const MzhSearchParams& p, hipStream_t stream);

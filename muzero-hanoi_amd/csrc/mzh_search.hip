@@ -30,14 +30,6 @@ struct __align__(128) MzhBlock {
 static_assert(sizeof(MzhBlock) == 128, "block layout");
 static_assert(__builtin_offsetof(MzhBlock, W) == 72, "block layout");
 
-// select-phase options (A/B-able in diagnostic builds): child-block prefetch one level ahead
-#ifndef MZH_SELECT_PF
-#define MZH_SELECT_PF 1
-#endif
-// next-level (N | X) word: 1 = cross-lane shuffle (measured faster), 0 = picked from the six words every lane loads
-#ifndef MZH_NX_SHFL
-#define MZH_NX_SHFL 1
-#endif
 
 // the root's 6 children live in LDS for the whole search (every simulation starts there)
 struct MzhRootBlk {
@@ -136,15 +128,12 @@ __device__ __forceinline__ double mzh_pow(double x, double e) {
   return pow(x, e);
 }
 
-// R = 32: one workgroup per CU (all 512 registers per lane); R = 16: two co-resident workgroups
-// per CU (<= 256 registers), so one workgroup's latency-bound tree phase overlaps the other's MFMAs.
-#ifndef MZH_PF16
-#define MZH_PF16 1  // 1: R = 16 also prefetches across the tree phase (needs the full register file: one workgroup per CU)
-#endif
+// One workgroup per CU (all 512 registers per lane): the next simulation's first weight chunks stay
+// in flight across the tree phase.  (Two co-resident 16-root workgroups per CU without that prefetch,
+// <= 256 registers and 16 cached path depths, measured 11% slower at 8,192 roots: DESIGN.md §3.)
 template <int R, bool REPLAY, bool OHL>
-__global__ __launch_bounds__(MZH_THREADS, R == 16 && !MZH_PF16 ? 2 : 1) void mzh_search_kernel(MzhNet net, MzhSearchParams p) {
+__global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, MzhSearchParams p) {
   constexpr int DC = SearchSmem<R>::DC;
-  constexpr bool PF = R == 32 || MZH_PF16;  // keep the next step's first weight chunks in flight across the tree phase
   extern __shared__ __align__(16) unsigned char smem_raw[];
   MlpSmem<R>& sm = *reinterpret_cast<MlpSmem<R>*>(smem_raw);
   SearchSmem<R>& st = *reinterpret_cast<SearchSmem<R>*>(smem_raw + sizeof(MlpSmem<R>));
@@ -221,7 +210,7 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 && !MZH_PF16 ? 2 : 1) void mzh
   if (tid < R && tid >= nvalid) sm.act[tid] = 0;  // rows beyond the batch: any valid one-hot index
   floatx4 fa[16], fb[16];
   float ba[4], bb[4];
-  if (!REPLAY && PF) mzh_mlp_fetch12<R>(sm, net, wave, lane, fa, ba, fb, bb);
+  if (!REPLAY) mzh_mlp_fetch12<R>(sm, net, wave, lane, fa, ba, fb, bb);
   __syncthreads();
 
   MZH_STAMP_DECL
@@ -262,7 +251,7 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 && !MZH_PF16 ? 2 : 1) void mzh
         // (unconditional loads -- a lane without a child re-reads a valid block -- so the
         // compiler can count outstanding loads and wait only for the ones a level needs)
         int pf0 = 0;
-        if (MZH_SELECT_PF) pf0 = *reinterpret_cast<const int*>(tb + (Xc >= 0 ? Xc : 0));
+        pf0 = *reinterpret_cast<const int*>(tb + (Xc >= 0 ? Xc : 0));
         int nx = __shfl((Nc & 0xFFFF) | (Xc << 16), (lane & ~7) + pick);
         int depth = 1, e = 0;
 
@@ -276,10 +265,6 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 && !MZH_PF16 ? 2 : 1) void mzh
           e = nx >> 16;
           const int Np = nx & 0xFFFF;
           const MzhBlock* b = tb + e;
-          // all six (N | X << 16) words (same cache line): the next level's block index is
-          // picked from registers instead of a cross-lane shuffle
-          const int4 n03 = *reinterpret_cast<const int4*>(&b->nx[0]);
-          const int2 n45 = *reinterpret_cast<const int2*>(&b->nx[4]);
           int nxc = *reinterpret_cast<const int*>(&b->nx[cs]);
           Rc = b->R[cs];
           Wc = b->W[cs];
@@ -287,9 +272,9 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 && !MZH_PF16 ? 2 : 1) void mzh
           if (c >= MZH_A) nxc = (int)0xFFFF0000;
           // retire the previous level's prefetch (older than this level's block loads, so no
           // extra wait) -- keeps it in flight inside the loop
-          if (MZH_SELECT_PF) asm volatile("" ::"v"(pf0));
+          asm volatile("" ::"v"(pf0));
           const int xc = nxc >> 16;
-          if (MZH_SELECT_PF) pf0 = *reinterpret_cast<const int*>(tb + (xc >= 0 ? xc : e));
+          pf0 = *reinterpret_cast<const int*>(tb + (xc >= 0 ? xc : e));
           Nc = nxc & 0xFFFF;
           MZH_LSTAMP(0);
           ucb = c < MZH_A ? mzh_ucb(Nc, Wc, Rc, (double)Pc, p.np1, table[Np], disc, has, mmin, den, dinv, inv)
@@ -301,16 +286,13 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 && !MZH_PF16 ? 2 : 1) void mzh
             path[r * PL + depth] = (uint16_t)(e * 8 + pick);
             if (depth < DC) st.pc[r][depth] = MzhPathEnt{Wc, Rc, Nc};
           }
-          if (MZH_NX_SHFL)
-            nx = __shfl(nxc, (lane & ~7) + pick);
-          else
-            nx = pick == 0 ? n03.x : pick == 1 ? n03.y : pick == 2 ? n03.z : pick == 3 ? n03.w : pick == 4 ? n45.x : n45.y;
+          nx = __shfl(nxc, (lane & ~7) + pick);
           depth++;
           MZH_LSTAMP(3);
         }
         MZH_LSTAMP_FLUSH(24);
         MZH_STAMP(30);
-        if (MZH_SELECT_PF) asm volatile("" ::"v"(pf0));
+        asm volatile("" ::"v"(pf0));
         if (c == 0) {
           st.depth[r] = depth;
           st.leafE[r] = e;
@@ -341,11 +323,7 @@ __global__ __launch_bounds__(MZH_THREADS, R == 16 && !MZH_PF16 ? 2 : 1) void mzh
     // ---------------- Phase 2: expand via the network (mcts.py:88-106) ----------------
     if (!REPLAY) {
       MZH_STAMP(19);
-      if (PF) {
-        mzh_mlp_recurrent_body<R, PF>(sm, net, wave, lane, fa, ba, fb, bb, OHL ? ohl : net.dyn0_onehot);
-      } else {
-        mzh_mlp_recurrent<R>(sm, net, wave, lane);
-      }
+      mzh_mlp_recurrent_body<R, true>(sm, net, wave, lane, fa, ba, fb, bb, OHL ? ohl : net.dyn0_onehot);
       MZH_STAMP(20);
     } else {
       if (tid < R * 8) {

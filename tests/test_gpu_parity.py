@@ -307,17 +307,6 @@ def test_search_deep_paths_replay(mzh, oracle, kernel):
     assert np.array_equal(o["sel_steps"], ref["sel_steps"])
 
 
-def test_selftest_register_reciprocal(mzh):
-    """The search kernels' RN(1/n) (v_rcp_f64 + one Newton step) equals IEEE 1/n for every n the
-    select/backup divisions can meet (N <= max_sims + 1 <= 32001; checked to 2^20)."""
-    from muzero_hanoi_amd import _lib
-
-    bad = torch.zeros(1, dtype=torch.int32, device=DEV)
-    _lib.check(_lib.lib().mzh_selftest(_lib.MZH_SELFTEST_RCP, 1 << 20, _lib.ptr(bad), _lib.stream_handle(bad.device)),
-               "mzh_selftest")
-    assert int(bad.item()) == 0
-
-
 # ------------------------------------------------------- BASELINE.json configs at full size
 def _sample_idx(B, seed):
     """first 16, last 16 and 16 random roots of a batch"""

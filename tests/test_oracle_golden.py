@@ -176,3 +176,14 @@ def test_replay_tree_bit_exact(oracle, case):
         L = out["latent_len"][b]
         want = g["latent"][b]
         assert list(out["latent"][b][:L]) == [int(v) for v in want[want >= 0]]
+
+
+@pytest.mark.parametrize("n", [3, 4, 7])
+def test_hanoi_solver_dropin_host(n):
+    """the scalar drop-in (host closed form) equals the reference's hanoi_solver on every state"""
+    from muzero_hanoi_amd.hanoi_utils import hanoi_solver
+
+    g = golden(f"solver_N{n}.npz")
+    for i, st in enumerate(_states(n)):
+        assert hanoi_solver(tuple(int(x) for x in st)) == g["moves"][i]
+        assert hanoi_solver(tuple(int(x) for x in st), 0) == g["moves_goal0"][i]
