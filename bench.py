@@ -205,10 +205,11 @@ def tree_bytes(sel_steps_sum, n_roots, S, expand_bytes):
 
 
 def kernel_name(kern, B):
+    """the search kernel mzh_api.hip choose_kernel() / pick_tile() launches for B roots"""
     kern_sel = kern if kern != "auto" else ("wave" if B >= 53248 else "wave16" if B > 8192 else "coop")
-    coop_rows = 32 if B > 4096 else 16  # mzh_api.hip choose_kernel() / pick_rows()
+    coop_rows = 32 if B > 4096 else 16
     return kern_sel, {"wave": "mzh_wave_kernel<2,{r},true>", "wave16": "mzh_wave_kernel<1,{r},true>",
-                      "coop": f"mzh_search_kernel<{coop_rows},{{r}},*>"}[kern_sel]
+                      "coop": f"mzh_search_kernel<{coop_rows},{{r}},*,true>"}[kern_sel]
 
 
 def main():

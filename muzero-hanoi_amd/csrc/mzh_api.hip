@@ -360,11 +360,14 @@ extern "C" int mzh_hanoi_solver(int n_disks, int goal_peg, int B, const uint8_t*
 }
 
 // ---- inference ----
-// roots (rows) per workgroup: 16 while that fits one workgroup per CU (B <= 4096), else 32 -- a
-// second round of 16-row workgroups costs more than the 32-row tiles (measured: 5,120 roots 1.05e8
-// vs 1.68e8 sims/s, 7,168 roots 1.46e8 vs 2.32e8; 4,096 roots 1.58e8 vs 1.34e8).
-// MZH_ROWS=16|32 in the environment forces a tile size (A/B experiments only).
-static int pick_rows(int B) {
+// roots (rows) per workgroup of the standalone inference kernels: 16 while that fits one workgroup
+// per CU (B <= 4096), else 32
+static int pick_rows(int B) { return B > 256 * 16 ? 32 : 16; }
+
+// cooperative search tile: 16 roots while that is one round of workgroups (B <= 4,096), else 32
+// roots (a second round of 16-root workgroups costs more than 32-root tiles).  MZH_ROWS=16|32 in the
+// environment forces one (A/B experiments only).
+static int pick_tile(int B) {
   static const int forced = [] {
     const char* v = getenv("MZH_ROWS");
     return v ? atoi(v) : 0;
@@ -409,9 +412,9 @@ extern "C" int mzh_recurrent_inference(mzh_engine* eng, int B, const float* h_in
 static const size_t kMaxLds = 163840;
 
 // kernel choice: the wave-independent kernel (mzh_wave.hip) with 32 roots per wave once the batch
-// gives >= 1024 waves (one per SIMD, two co-resident per SIMD at 65k roots), with 16 roots per wave
-// for mid-size batches (>= 1024 such waves), else the cooperative kernel (mzh_search.hip) whose 4
-// waves share one 32-root MLP tile.  MZH_FLAG_KERNEL_* (or MZH_KERNEL=coop|wave|wave16) force one.
+// gives two such waves per SIMD, with 16 roots per wave for mid-size batches (>= 1024 such waves),
+// else the cooperative kernel (mzh_search.hip) whose 4 waves split every MLP layer of one 16- or
+// 32-root tile.  MZH_FLAG_KERNEL_* (or MZH_KERNEL=coop|wave|wave16) force one.
 static const int kWaveMinRoots = 53248, kWave16MinRoots = 8193;  // measured crossovers
 struct KernelChoice {
   bool wave;
@@ -452,7 +455,7 @@ static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream s
     return fail(MZH_ERR_ARG, "stochastic action selection needs action_u");
   const KernelChoice kc = choose_kernel(a->B, a->flags);
   const bool wave = kc.wave;
-  int R = pick_rows(a->B);
+  int R = pick_tile(a->B);
   if (wave) {
     if (mzh_wave_smem_bytes(a->n_sims, kc.nt) > kMaxLds)
       return fail(MZH_ERR_CAPACITY, "n_sims=%d exceeds the wave kernel's LDS table budget", a->n_sims);

@@ -340,6 +340,11 @@ __device__ __forceinline__ void mzh_run_jobs(const MzhJob* jobs, int KB, const f
 // fetches the NEXT chunk's weights (and biases) while its MFMAs consume the current one; loads stay
 // in flight across __syncthreads (no LDS-DMA is outstanding, so the barrier does not drain them).
 // ------------------------------------------------------------------------------------------
+// the MLP's phase barrier (a functor, so a kernel can supply a sub-group barrier)
+struct MzhSyncBar {
+  __device__ __forceinline__ void operator()() const { __syncthreads(); }
+};
+
 struct MzhChunk {
   const float4* w[4];
   const float* bias[4];  // already offset to the tile's first column
@@ -363,20 +368,24 @@ __device__ __forceinline__ MzhChunk mzh_chunk(const MzhLayer& L, int nt0, int nj
   return c;
 }
 
+// loads issued in consumption order (k-block major, the tiles of a k-block together), biases last:
+// the MFMAs of k-block 0 wait only for the oldest NJ fragments, not for the whole chunk
 template <int NJ, int KB, bool ALL = false>
 __device__ __forceinline__ void mzh_fetch(floatx4* f, float* bv, const MzhChunk& c, int lane) {
   static_assert(NJ * KB <= 16, "chunk too large");
 #pragma unroll
-  for (int q = 0; q < NJ; ++q) {
-    if (ALL || q < c.nj) {
+  for (int kb = 0; kb < KB; ++kb) {
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
+    for (int q = 0; q < NJ; ++q) {
+      if (ALL || q < c.nj) {
         const float4 t = c.w[q][kb * 64 + lane];
         f[q * KB + kb] = floatx4{t.x, t.y, t.z, t.w};
       }
-      bv[q] = c.bias[q][lane & 15];
     }
   }
+#pragma unroll
+  for (int q = 0; q < NJ; ++q)
+    if (ALL || q < c.nj) bv[q] = c.bias[q][lane & 15];
 }
 
 // acc = A[rows][0:16KB] . W-tiles ; epilogue (+onehot) + bias (+relu) -> LDS
@@ -391,20 +400,31 @@ __device__ __forceinline__ void mzh_mma_store(const floatx4* f, const float* bv,
   for (int q = 0; q < NJ; ++q)
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[q][m] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // A operands double-buffered one k-block ahead: block kb + 1's LDS reads are issued before block
+  // kb's MFMAs (pinned by the scheduling barrier), so a K = 256 chain does not wait on LDS latency
+  // between its MFMAs
+  float a[2][4][MT];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) a[0][j][m] = A[(m * 16 + r) * lda + j * 4 + g];
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
+    if (kb + 1 < KB) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) a[(kb + 1) & 1][j][m] = A[(m * 16 + r) * lda + (kb + 1) * 16 + j * 4 + g];
+    }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int k = kb * 16 + j * 4 + g;
-      float a[MT];
-#pragma unroll
-      for (int m = 0; m < MT; ++m) a[m] = A[(m * 16 + r) * lda + k];
 #pragma unroll
       for (int q = 0; q < NJ; ++q) {
         if (ALL || q < c.nj) {
 #pragma unroll
           for (int m = 0; m < MT; ++m)
-            acc[q][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], f[q * KB + kb][j], acc[q][m], 0, 0, 0);
+            acc[q][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kb & 1][j][m], f[q * KB + kb][j], acc[q][m], 0, 0, 0);
         }
       }
     }
@@ -481,11 +501,8 @@ __device__ __forceinline__ void mzh_normalize_par(const float* src, float* dst, 
 // interleaved on the same lanes (independent chains), the policy softmax alongside.  Lane q owns
 // logits k = q + 8i; max / exp / divide are lane-parallel, and both 33-term sums use the fixed
 // order of sum8_tree in the oracle: sequential per-lane partials combined by the DPP tree.
-template <int R>
-__device__ __forceinline__ void mzh_heads_par(MlpSmem<R>& sm, float* scratch, int support, bool recurrent, int tid) {
-  (void)scratch;
-  const int row = tid >> 3, q = tid & 7;  // 32 rows of 8 lanes over 256 threads
-  if (row >= R) return;
+template <int R, class SM>
+__device__ __forceinline__ void mzh_heads_row(SM& sm, int row, int q, int support, bool recurrent) {
   const float lg = q < MZH_A ? sm.lpol[row * MZH_LDPOL + q] : -__builtin_inff();
   if (support == 1) {
     if (q == 0) {
@@ -566,24 +583,34 @@ __device__ __forceinline__ void mzh_heads_par(MlpSmem<R>& sm, float* scratch, in
   }
 }
 
+// all rows: 8 lanes per row, row = tid / 8 (32 rows over 256 threads)
+template <int R, class SM>
+__device__ __forceinline__ void mzh_heads_par(SM& sm, int support, bool recurrent, int tid) {
+  const int row = tid >> 3, q = tid & 7;
+  if (row < R) mzh_heads_row<R>(sm, row, q, support, recurrent);
+}
+
 // The per-wave chunk schedule of the prediction function (networks.py:140-150) on sm.x:
 //   C5/C6: pol0 (waves 0,1) or val0 (waves 2,3), 4 tiles each;  C7: pol2 (wave 0) / val2 (waves 1..)
-template <int R>
-__device__ __forceinline__ MzhChunk mzh_pred_chunk(MlpSmem<R>& sm, const MzhNet& net, int wave, int c) {
+template <int R, class SM>
+__device__ __forceinline__ MzhChunk mzh_pred_chunk(SM& sm, const MzhNet& net, int wave, int c) {
   const int id0 = wave * 8 + c * 4;
   return id0 >= 16 ? mzh_chunk(net.val0, id0 - 16, 4, sm.hidV, MZH_LD256)
                    : mzh_chunk(net.pol0, id0, 4, sm.hidP, MZH_LD256);
 }
-template <int R>
-__device__ __forceinline__ MzhChunk mzh_head_chunk(MlpSmem<R>& sm, const MzhNet& net, int wave) {
+template <int R, class SM>
+__device__ __forceinline__ MzhChunk mzh_head_chunk(SM& sm, const MzhNet& net, int wave) {
   if (wave == 0) return mzh_chunk(net.pol2, 0, 1, sm.lpol, MZH_LDPOL);
   return mzh_chunk(net.val2, wave - 1 < net.val2.nt ? wave - 1 : 0, wave - 1 < net.val2.nt ? 1 : 0, sm.lval, MZH_LDSUP);
 }
+// waves with a pol2 / val2 tile: all four for 33-bin heads (N2 = 3), waves 0-1 for scalar heads
+template <int N2>
+__device__ __forceinline__ bool mzh_has_head_tile(int wave) { return wave <= N2; }
 
 // nj consecutive tiles of the prediction hidden layers' 32-tile strip (tiles 0-15: pol0 -> hidP,
 // 16-31: val0 -> hidV; both read the normalised latent), starting at strip tile t0
-template <int R>
-__device__ __forceinline__ MzhChunk mzh_pred_tiles(MlpSmem<R>& sm, const MzhNet& net, int t0, int nj) {
+template <int R, class SM>
+__device__ __forceinline__ MzhChunk mzh_pred_tiles(SM& sm, const MzhNet& net, int t0, int nj) {
   MzhChunk c;
   c.ldo = MZH_LD256;
   c.nj = nj;
@@ -602,8 +629,8 @@ __device__ __forceinline__ MzhChunk mzh_pred_tiles(MlpSmem<R>& sm, const MzhNet&
 }
 
 // initial_inference (networks.py:71-94): sm.x holds obs rows zero-padded to 16*rep0.kb
-template <int R>
-__device__ void mzh_mlp_initial(MlpSmem<R>& sm, const MzhNet& net, int wave_in, int lane) {
+template <int R, class SM, class BAR = MzhSyncBar>
+__device__ void mzh_mlp_initial(SM& sm, const MzhNet& net, int wave_in, int lane, BAR bar = BAR{}) {
   constexpr int MT = R / 16;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(wave_in);
@@ -615,7 +642,7 @@ __device__ void mzh_mlp_initial(MlpSmem<R>& sm, const MzhNet& net, int wave_in, 
     for (int q = 0; q < 4; ++q) jobs[q] = mzh_job(sm.x, MZH_LD64, net.rep0, wave * 4 + q, sm.hidP, MZH_LD256, 1);
     mzh_run_jobs<MT, 4>(jobs, net.rep0.kb, nullptr, nullptr, lane);
   }
-  __syncthreads();
+  bar();
   {  // rep2: 4 tiles, 1 per wave
     MzhJob job = mzh_job(sm.hidP, MZH_LD256, net.rep2, wave, sm.hraw, MZH_LD64, 0);
     mzh_run_jobs<MT, 1>(&job, net.rep2.kb, nullptr, nullptr, lane);
@@ -624,17 +651,17 @@ __device__ void mzh_mlp_initial(MlpSmem<R>& sm, const MzhNet& net, int wave_in, 
   const MzhChunk c7 = mzh_head_chunk<R>(sm, net, wave);
   mzh_fetch<4, 4, true>(fa, ba, c5, lane);
   mzh_fetch<4, 4, true>(fb, bb, c6, lane);
-  __syncthreads();
+  bar();
   mzh_normalize_par<R>(sm.hraw, sm.x, tid);
-  __syncthreads();
+  bar();
   mzh_mma_store<MT, 4, 4, true>(fa, ba, c5, sm.x, MZH_LD64, true, nullptr, lane);
   mzh_fetch<1, 16>(fa, ba, c7, lane);
   mzh_mma_store<MT, 4, 4, true>(fb, bb, c6, sm.x, MZH_LD64, true, nullptr, lane);
-  __syncthreads();
+  bar();
   mzh_mma_store<MT, 1, 16>(fa, ba, c7, c7.out[0] == sm.lpol ? sm.hidP : sm.hidV, MZH_LD256, false, nullptr, lane);
-  __syncthreads();
-  mzh_heads_par<R>(sm, sm.hidR, net.support, false, tid);
-  __syncthreads();
+  bar();
+  mzh_heads_par<R>(sm, net.support, false, tid);
+  bar();
 }
 
 // recurrent_inference (networks.py:96-138), split so the first two chunks' weights (dyn0, dyn2)
@@ -643,18 +670,20 @@ __device__ void mzh_mlp_initial(MlpSmem<R>& sm, const MzhNet& net, int wave_in, 
 //   mzh_mlp_recurrent_body<R, NEXT> : the MLP; with NEXT it re-issues fetch12 for the next step
 // Input: sm.x = parent latents, sm.act = actions.  Output: sm.x = normalised new latent,
 // sm.pi / sm.value / sm.reward.
-template <int R>
-__device__ __forceinline__ void mzh_mlp_fetch12(MlpSmem<R>& sm, const MzhNet& net, int wave_in, int lane, floatx4* fa,
+template <int R, class SM>
+__device__ __forceinline__ void mzh_mlp_fetch12(SM& sm, const MzhNet& net, int wave_in, int lane, floatx4* fa,
                                                 float* ba, floatx4* fb, float* bb) {
   const int wave = __builtin_amdgcn_readfirstlane(wave_in);
   mzh_fetch<4, 4, true>(fa, ba, mzh_chunk(net.dyn0, wave * 4, 4, sm.hidP, MZH_LD256), lane);
   mzh_fetch<1, 16, true>(fb, bb, mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64), lane);
 }
 
-template <int R, bool NEXT>
-__device__ __forceinline__ void mzh_mlp_recurrent_body(MlpSmem<R>& sm, const MzhNet& net, int wave_in, int lane,
+// N2 = reward / value layer-2 tiles (3: 33-bin support, 1: scalar); HEADS: finish with the heads on
+// all rows (standalone inference) -- the search kernel runs each root's heads itself.
+template <int R, bool NEXT, int N2, bool HEADS, class SM, class BAR = MzhSyncBar>
+__device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net, int wave_in, int lane,
                                                        floatx4* fa, float* ba, floatx4* fb, float* bb,
-                                                       const float* onehot) {
+                                                       const float* onehot, BAR bar = BAR{}) {
   constexpr int MT = R / 16;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(wave_in);  // wave-uniform -> chunk descriptors in SGPRs
@@ -675,22 +704,21 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(MlpSmem<R>& sm, const Mzh
                             lane);  // dyn0 + one-hot + bias, relu
   }
   MZH_STAMP(1);
-  __syncthreads();
+  bar();
   mzh_fetch<4, 4, true>(fa, ba, mzh_chunk(net.rwd0, wave * 4, 4, sm.hidR, MZH_LD256), lane);
   MZH_STAMP(2);
   mzh_mma_store<MT, 1, 16, true>(fb, bb, mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64), sm.hidP, MZH_LD256, false,
                                  nullptr, lane);  // dyn2 -> h'
   MZH_STAMP(3);
-  __syncthreads();
-  // Phase B (after rwd0) balances rwd2 against the prediction hidden layers: with n2 = rwd2 tiles
-  // (3 for support 33), waves w < n2 run one rwd2 tile (K = 256, 4 units) + n2 + 4 prediction
-  // tiles (K = 64, 1 unit each), the others n2 + 8 prediction tiles -- 8 + n2 units per wave.
-  const int n2 = net.rwd2.nt;
-  const bool r2 = wave < n2;
-  const int P1 = r2 ? wave * (n2 + 4) : n2 * (n2 + 4) + (wave - n2) * (n2 + 8);
+  bar();
+  // Phase B (after rwd0) balances rwd2 against the prediction hidden layers: waves w < N2 run one
+  // rwd2 tile (K = 256, 4 units) + N2 + 4 prediction tiles (K = 64, 1 unit each), the others N2 + 8
+  // prediction tiles -- 8 + N2 units per wave.
+  const bool r2 = wave < N2;
+  const int P1 = r2 ? wave * (N2 + 4) : N2 * (N2 + 4) + (wave - N2) * (N2 + 8);
   const int P2 = P1 + (r2 ? 0 : 4), P3 = P2 + 4;
   if (r2)
-    mzh_fetch<1, 16>(fb, bb, mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP), lane);
+    mzh_fetch<1, 16, true>(fb, bb, mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP), lane);
   else
     mzh_fetch<4, 4, true>(fb, bb, mzh_pred_tiles<R>(sm, net, P1, 4), lane);
   MZH_STAMP(4);
@@ -699,37 +727,43 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(MlpSmem<R>& sm, const Mzh
   mzh_mma_store<MT, 4, 4, true>(fa, ba, mzh_chunk(net.rwd0, wave * 4, 4, sm.hidR, MZH_LD256), sm.hraw, MZH_LD64, true,
                           nullptr, lane);  // rwd0 on h' (networks.py:132)
   MZH_STAMP(6);
-  __syncthreads();
+  bar();
   mzh_fetch<4, 4, true>(fa, ba, mzh_pred_tiles<R>(sm, net, P2, 4), lane);
   MZH_STAMP(7);
   if (r2)
-    mzh_mma_store<MT, 1, 16>(fb, bb, mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP), sm.hidR, MZH_LD256, false,
-                             nullptr, lane);  // rwd2 -> reward logits
+    mzh_mma_store<MT, 1, 16, true>(fb, bb, mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP), sm.hidR, MZH_LD256, false,
+                                   nullptr, lane);  // rwd2 -> reward logits
   else
     mzh_mma_store<MT, 4, 4, true>(fb, bb, mzh_pred_tiles<R>(sm, net, P1, 4), sm.x, MZH_LD64, true, nullptr, lane);
-  mzh_fetch<3, 4>(fb, bb, mzh_pred_tiles<R>(sm, net, P3, n2), lane);
+  mzh_fetch<N2, 4, true>(fb, bb, mzh_pred_tiles<R>(sm, net, P3, N2), lane);
   MZH_STAMP(8);
   mzh_mma_store<MT, 4, 4, true>(fa, ba, mzh_pred_tiles<R>(sm, net, P2, 4), sm.x, MZH_LD64, true, nullptr, lane);
-  mzh_fetch<1, 16>(fa, ba, mzh_head_chunk<R>(sm, net, wave), lane);
-  mzh_mma_store<MT, 3, 4>(fb, bb, mzh_pred_tiles<R>(sm, net, P3, n2), sm.x, MZH_LD64, true, nullptr, lane);
+  const bool ht = mzh_has_head_tile<N2>(wave);
+  if (ht) mzh_fetch<1, 16, true>(fa, ba, mzh_head_chunk<R>(sm, net, wave), lane);
+  mzh_mma_store<MT, N2, 4, true>(fb, bb, mzh_pred_tiles<R>(sm, net, P3, N2), sm.x, MZH_LD64, true, nullptr, lane);
   MZH_STAMP(9);
-  __syncthreads();
-  mzh_mma_store<MT, 1, 16>(fa, ba, mzh_head_chunk<R>(sm, net, wave), wave == 0 ? sm.hidP : sm.hidV, MZH_LD256,
-                           false, nullptr, lane);  // pol2 / val2
+  bar();
+  if (ht)
+    mzh_mma_store<MT, 1, 16, true>(fa, ba, mzh_head_chunk<R>(sm, net, wave), wave == 0 ? sm.hidP : sm.hidV, MZH_LD256,
+                                   false, nullptr, lane);  // pol2 / val2
   if (NEXT) mzh_mlp_fetch12<R>(sm, net, wave, lane, fa, ba, fb, bb);  // next step's first chunks
   MZH_STAMP(10);
-  __syncthreads();
-  mzh_heads_par<R>(sm, sm.hidR, net.support, true, tid);
-  MZH_STAMP(11);
-  __syncthreads();
+  bar();
+  if (HEADS) {
+    mzh_heads_par<R>(sm, net.support, true, tid);
+    MZH_STAMP(11);
+    bar();
+  }
   MZH_STAMP(12);
 }
-
 
 template <int R>
 __device__ void mzh_mlp_recurrent(MlpSmem<R>& sm, const MzhNet& net, int wave, int lane) {
   floatx4 fa[16], fb[16];
   float ba[4], bb[4];
   mzh_mlp_fetch12<R>(sm, net, wave, lane, fa, ba, fb, bb);
-  mzh_mlp_recurrent_body<R, false>(sm, net, wave, lane, fa, ba, fb, bb, net.dyn0_onehot);
+  if (net.support == 33)
+    mzh_mlp_recurrent_body<R, false, 3, true>(sm, net, wave, lane, fa, ba, fb, bb, net.dyn0_onehot);
+  else
+    mzh_mlp_recurrent_body<R, false, 1, true>(sm, net, wave, lane, fa, ba, fb, bb, net.dyn0_onehot);
 }

@@ -1,0 +1,386 @@
+// mzh_tree.h -- the search tree on the device: layout in HBM / LDS and the per-root select,
+// expand/backup and result steps of the cooperative search kernels (mzh_search.hip,
+// mzh_split.hip).  Each root is owned by one aligned 8-lane group (lane c = child slot c).
+//
+// Reference: MCTS/mcts.py:34-176 (run_mcts, generate_play_policy), MCTS/node.py:30-136
+// (expand / backup / best_child / child_Q / child_U), MCTS/utils_mcts.py:1-16 (MinMaxStats).
+#pragma once
+#include "mzh_device.h"
+#include "mzh_internal.h"
+
+// ------------------------------------------------------------------------------------------
+// tree block: the 6 children of one expanded node in exactly one 128-byte cache line, so a
+// selection level touches one line (L2-resident hot path)
+// ------------------------------------------------------------------------------------------
+struct MzhNX {
+  uint16_t N;  // child visit count (node.py:21)
+  int16_t X;   // expanded-node index of the child, -1 = not expanded (node.py:19 is_expanded)
+};
+struct __align__(128) MzhBlock {
+  MzhNX nx[6];  // N and X adjacent: one dword load per child in selection
+  float R[6];   // child reward (python float of an fp32 value, node.py:25)
+  float P[6];   // child prior, fp32 (node.py:16)
+  double W[6];  // child summed value, fp64 (node.py:22)
+  uint32_t pad[2];
+};
+static_assert(sizeof(MzhBlock) == 128, "block layout");
+static_assert(__builtin_offsetof(MzhBlock, W) == 72, "block layout");
+
+
+// the root's 6 children live in LDS for the whole search (every simulation starts there)
+struct MzhRootBlk {
+  double W[8];
+  double P64[8];  // prior as fp64: Dirichlet-mixed (np.float64) or the widened fp32 prior
+  float R[8];
+  int N[8];
+  int X[8];
+};
+
+// snapshot of the chosen child's statistics at each depth of the current simulation's path,
+// taken during selection so the backup needs no dependent global loads (depth < DC)
+struct MzhPathEnt {
+  double W;
+  float R;
+  int N;
+};
+
+template <int R, int DC_>
+struct SearchSmem {
+  static constexpr int DC = DC_;
+  MzhRootBlk root[R];
+  MzhPathEnt pc[R][DC];
+  double bval[R][DC];  // value added at each cached path depth (backup value chain)
+  double rootW[R];
+  double mm[R][4];  // MinMaxStats (maximum, minimum) + normaliser (max - min, RN(1/(max - min)))
+  int rootN[R];
+  int firstTie[R];
+  int extra[R];
+  int depth[R];
+  int leafE[R];
+  int leafA[R];
+  int steps[R];
+  int pad_[R];
+};
+
+// a / b correctly rounded from y = RN(1/b) (Markstein: q = RN(a*y) is within one ulp, the fma
+// residual is exact, and one correction step rounds to RN(a/b)); 3 fp64 ops instead of the
+// ~12-op div_scale/rcp/fmas/fixup sequence on the select chain.  Equal to `a / b` for every
+// finite non-subnormal quotient; checked against true division in tests/test_markstein.py.
+__device__ __forceinline__ double mzh_div(double a, double b, double y) {
+  const double q = a * y;
+  const double r = __builtin_fma(-q, b, a);
+  return __builtin_fma(r, y, q);
+}
+
+// MinMaxStats.normalize (utils_mcts.py:12-16) with den = max - min, dinv = RN(1/den)
+__device__ __forceinline__ double mzh_normalize(double v, bool has, double mn, double den, double dinv) {
+  return has ? mzh_div(v - mn, den, dinv) : v;
+}
+
+// ucb = fl32(Q) + fl32(U) for one child (node.py:90-123); `tnp` = table[N_parent], inv[k] = RN(1/k)
+__device__ __forceinline__ float mzh_ucb(int Nc, double Wc, float Rc, double P64, bool p64_semantics, double tnp,
+                                         double disc, bool has, double mn, double den, double dinv,
+                                         const double* inv) {
+  float q32 = 0.0f;
+  if (Nc > 0) q32 = (float)mzh_normalize((double)Rc + disc * mzh_div(Wc, (double)Nc, inv[Nc]), has, mn, den, dinv);
+  const double w = mzh_div(tnp, (double)(Nc + 1), inv[Nc + 1]);
+  // np.float64 priors (Dirichlet-mixed root) or NumPy-1 promotion: fl32(fl64(prior * w));
+  // NumPy-2 with np.float32 priors: fl32(prior * fl32(w))
+  const float u32 = p64_semantics ? (float)(P64 * w) : (float)P64 * (float)w;
+  return q32 + u32;
+}
+
+// MinMaxStats update with the select-side normaliser precomputed (den, RN(1/den))
+__device__ __forceinline__ void mzh_mm_set(double* mm, double mx, double mn) {
+  mm[0] = mx;
+  mm[1] = mn;
+  mm[2] = mx - mn;
+  mm[3] = mx > mn ? 1.0 / (mx - mn) : 0.0;
+}
+
+// argmax over the 6 children held by the 8-lane group, with the reference's tie handling:
+// np.random.choice(argmax set) -- the first 6-way tie takes the host-drawn index, any other tie
+// is counted (RNG-stream divergence) and resolved to the lowest index.  Branch-free; every lane
+// of the group returns the same pick.
+__device__ __forceinline__ int mzh_group_pick(float ucb, int c, int lane, int tie, int& firstTie, int& extra) {
+  const float m = mzh_max8(ucb);
+  const unsigned long long bal = __ballot(c < MZH_A && ucb == m);
+  const unsigned mask = (unsigned)(bal >> (lane & ~7)) & 0x3Fu;
+  const int cnt = __popc(mask);
+  const int first = __ffs(mask) - 1;
+  const bool six = (cnt == MZH_A) & (firstTie == 0);
+  extra += ((cnt > 1) & !six) ? 1 : 0;
+  firstTie |= six ? 1 : 0;
+  return six ? tie : first;
+}
+
+// x ** e with numpy semantics for the exponents generate_play_policy can produce
+__device__ __forceinline__ double mzh_pow(double x, double e) {
+  if (e == __builtin_rint(e) && e >= 1.0 && e <= 5.0) {
+    double r = x;
+    for (int i = 1; i < (int)e; ++i) r = r * x;
+    return r;
+  }
+  return pow(x, e);
+}
+
+
+// Per-root steps over one workgroup's trees.  R roots (st / sm rows 0..R-1), DC path depths cached
+// in LDS, `path` = [R][S + 1] selection slots.  SM: the MLP storage holding each root's row of the
+// MLP input / output (x, act, pi, value, reward).
+template <int R, int DC, bool REPLAY, class SM>
+struct MzhTree {
+  const MzhSearchParams& p;
+  SearchSmem<R, DC>& st;
+  SM& sm;
+  uint16_t* path;
+  const double* table;
+  const double* inv;
+  int root0, PL, lane;
+  double disc;
+  bool noised;
+
+  __device__ __forceinline__ void select(const int r, const int c, const int s) {
+    const MzhBlock* tb = reinterpret_cast<const MzhBlock*>(p.tree) + (size_t)(root0 + r) * p.E;
+    const double mmax = st.mm[r][0], mmin = st.mm[r][1], den = st.mm[r][2], dinv = st.mm[r][3];
+    const bool has = mmax > mmin;
+    int firstTie = st.firstTie[r];
+    int extra = st.extra[r];
+    const int tie = p.tie_idx ? p.tie_idx[root0 + r] : 0;
+    // level 0: the root block (LDS)
+    int Nc = 0, Xc = -1;
+    double Wc = 0.0;
+    float Rc = 0.0f;
+    float ucb = -__builtin_inff();
+    if (c < MZH_A) {
+      const MzhRootBlk& rb = st.root[r];
+      Nc = rb.N[c];
+      Xc = rb.X[c];
+      Wc = rb.W[c];
+      Rc = rb.R[c];
+      ucb = mzh_ucb(Nc, Wc, Rc, rb.P64[c], noised || p.np1, table[st.rootN[r]], disc, has, mmin, den, dinv, inv);
+    }
+    int pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
+    // the picking lane records the path entry and its own statistics; one shuffle of the
+    // packed (N | X << 16) word moves the selection on
+    if (c == pick) {
+      path[r * PL] = (uint16_t)pick;
+      st.pc[r][0] = MzhPathEnt{Wc, Rc, Nc};
+    }
+    // every lane prefetches its own child's block (the selection's next level is one of
+    // them): the block's cache lines are in flight while this level's UCB/argmax completes
+    // (unconditional loads -- a lane without a child re-reads a valid block -- so the
+    // compiler can count outstanding loads and wait only for the ones a level needs)
+    int pf0 = *reinterpret_cast<const int*>(tb + (Xc >= 0 ? Xc : 0));
+    int nx = __shfl((Nc & 0xFFFF) | (Xc << 16), (lane & ~7) + pick);
+    int depth = 1, e = 0;
+
+    // deeper levels: tree blocks in HBM (L2); lanes 6, 7 re-read slot 5 and act as
+    // unexpanded, unvisited pads (N = 0, X = -1)
+    const int cs = c < MZH_A ? c : MZH_A - 1;
+    while ((nx >> 16) >= 0) {
+      e = nx >> 16;
+      const int Np = nx & 0xFFFF;
+      const MzhBlock* b = tb + e;
+      int nxc = *reinterpret_cast<const int*>(&b->nx[cs]);
+      Rc = b->R[cs];
+      Wc = b->W[cs];
+      const float Pc = b->P[cs];
+      if (c >= MZH_A) nxc = (int)0xFFFF0000;
+      // retire the previous level's prefetch (older than this level's block loads, so no
+      // extra wait) -- keeps it in flight inside the loop
+      asm volatile("" ::"v"(pf0));
+      const int xc = nxc >> 16;
+      pf0 = *reinterpret_cast<const int*>(tb + (xc >= 0 ? xc : e));
+      Nc = nxc & 0xFFFF;
+      ucb = c < MZH_A ? mzh_ucb(Nc, Wc, Rc, (double)Pc, p.np1, table[Np], disc, has, mmin, den, dinv, inv)
+                      : -__builtin_inff();
+      pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
+      if (c == pick) {
+        path[r * PL + depth] = (uint16_t)(e * 8 + pick);
+        if (depth < DC) st.pc[r][depth] = MzhPathEnt{Wc, Rc, Nc};
+      }
+      nx = __shfl(nxc, (lane & ~7) + pick);
+      depth++;
+    }
+    asm volatile("" ::"v"(pf0));
+    if (c == 0) {
+      st.depth[r] = depth;
+      st.leafE[r] = e;
+      st.leafA[r] = pick;
+      st.steps[r] += depth;
+      st.firstTie[r] = firstTie;
+      st.extra[r] = extra;
+    }
+    if (!REPLAY) {
+      // MLP input: the leaf's parent latent (mcts.py:89-92).  The node expanded by the previous
+      // simulation (index s; the root at s = 0) is still in sm.x as that MLP's output.
+      if (e != s) {
+        const floatx4* hsrc = reinterpret_cast<const floatx4*>(p.htree) + ((size_t)(root0 + r) * p.E + e) * 16 + c * 2;
+        const floatx4 h0 = hsrc[0], h1 = hsrc[1];
+        float* d = &sm.x[r * MZH_LD64 + c * 8];
+        d[0] = h0[0]; d[1] = h0[1]; d[2] = h0[2]; d[3] = h0[3];
+        d[4] = h1[0]; d[5] = h1[1]; d[6] = h1[2]; d[7] = h1[3];
+      }
+      if (c == 0) sm.act[r] = pick;
+    }
+  }
+
+  // ---------------- expand bookkeeping + backup (node.py:30-70) of simulation s ----------------
+  // Lane 0 of the root's group runs the value chain leaf -> root (two fp64 ops per level, the only
+  // serial part); the 8 lanes then update the cached path nodes in parallel and reduce the
+  // MinMaxStats candidates (max/min are exact and order-free).
+  __device__ __forceinline__ void backup(const int r, const int c, const int s) {
+    MzhBlock* tb = reinterpret_cast<MzhBlock*>(p.tree) + (size_t)(root0 + r) * p.E;
+    MzhRootBlk& rb = st.root[r];
+    const int enew = s + 1;
+    if (!REPLAY) {
+      // the new node's latent (read back when one of its children is expanded -- usually
+      // within a few simulations on the deepening path, so it stays cacheable)
+      const float* src = &sm.x[r * MZH_LD64 + c * 8];
+      floatx4* dst = reinterpret_cast<floatx4*>(p.htree) + ((size_t)(root0 + r) * p.E + enew) * 16 + c * 2;
+      const floatx4 v0 = {src[0], src[1], src[2], src[3]}, v1 = {src[4], src[5], src[6], src[7]};
+      dst[0] = v0;
+      dst[1] = v1;
+    }
+    MzhBlock* nb = tb + enew;  // the new expanded node's 6 children (node.py:44-49)
+    if (c < MZH_A) {
+      *reinterpret_cast<uint32_t*>(&nb->nx[c]) = 0xFFFF0000u;  // N = 0, X = -1
+      nb->R[c] = 0.0f;
+      nb->P[c] = sm.pi[r * 8 + c];
+      nb->W[c] = 0.0;
+    }
+    const int le = st.leafE[r], la = st.leafA[r], depth = st.depth[r];
+    const float rew = sm.reward[r];
+    double lmax = -__builtin_inf(), lmin = __builtin_inf();
+    if (c == 0) {
+      if (le == 0) {
+        rb.X[la] = enew;
+        rb.R[la] = rew;
+      } else {
+        tb[le].nx[la].X = (int16_t)enew;
+        tb[le].R[la] = rew;
+      }
+      double v = (double)sm.value[r];
+      int j = depth - 1;
+      for (; j >= DC; --j) {  // beyond the LDS path cache (rare): update here from HBM
+        const int slot = path[r * PL + j];
+        const int e = slot >> 3, a = slot & 7;
+        const double rw = (j == depth - 1) ? (double)rew : (double)tb[e].R[a];
+        const double W = tb[e].W[a] + v;
+        const int N = tb[e].nx[a].N + 1;
+        tb[e].W[a] = W;
+        tb[e].nx[a].N = (uint16_t)N;
+        const double q = rw + disc * mzh_div(W, (double)N, inv[N]);
+        lmax = q > lmax ? q : lmax;
+        lmin = q < lmin ? q : lmin;
+        v = rw + disc * v;
+      }
+      if (j == depth - 1 && j >= 0) {  // the leaf (its reward was just set)
+        st.bval[r][j] = v;
+        v = (double)rew + disc * v;
+        --j;
+      }
+#pragma unroll 4
+      for (; j >= 0; --j) {
+        st.bval[r][j] = v;
+        v = (double)st.pc[r][j].R + disc * v;
+      }
+      const double W = st.rootW[r] + v;
+      const int N = st.rootN[r] + 1;
+      st.rootW[r] = W;
+      st.rootN[r] = N;
+      const double q = 0.0 + disc * mzh_div(W, (double)N, inv[N]);  // root rwd = 0.0
+      lmax = q > lmax ? q : lmax;
+      lmin = q < lmin ? q : lmin;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int jmax = depth < DC ? depth : DC;
+    for (int j = c; j < jmax; j += 8) {
+      const int slot = path[r * PL + j];
+      const int e = slot >> 3, a = slot & 7;
+      const MzhPathEnt pe = st.pc[r][j];
+      const double rw = (j == depth - 1) ? (double)rew : (double)pe.R;
+      const double W = pe.W + st.bval[r][j];
+      const int N = pe.N + 1;
+      if (e == 0) {
+        rb.W[a] = W;
+        rb.N[a] = N;
+      } else {
+        tb[e].W[a] = W;
+        tb[e].nx[a].N = (uint16_t)N;
+      }
+      const double q = rw + disc * mzh_div(W, (double)N, inv[N]);
+      lmax = q > lmax ? q : lmax;
+      lmin = q < lmin ? q : lmin;
+    }
+    mzh_maxmin8d(lmax, lmin);
+    if (c == 0) {
+      const double mx = st.mm[r][0], mn = st.mm[r][1];
+      mzh_mm_set(st.mm[r], lmax > mx ? lmax : mx, lmin < mn ? lmin : mn);
+    }
+  }
+
+  // ---------------- results of root r (mcts.py:111-126, 154-176), one lane ----------------
+  __device__ __forceinline__ void results(const int r) {
+    const int root = root0 + r;
+    int vis[MZH_A];
+    for (int a = 0; a < MZH_A; ++a) {
+      vis[a] = st.root[r].N[a];
+      p.visits[(size_t)root * MZH_A + a] = vis[a];
+    }
+    if (p.root_q) p.root_q[root] = st.rootN[r] == 0 ? 0.0 : st.rootW[r] / (double)st.rootN[r];
+    if (p.minmax_out) {
+      p.minmax_out[2 * root] = st.mm[r][0];
+      p.minmax_out[2 * root + 1] = st.mm[r][1];
+    }
+    if (p.extra_ties) p.extra_ties[root] = st.extra[r];
+    if (p.sel_steps) p.sel_steps[root] = st.steps[r];
+    if (p.latent && p.S > 0) {
+      const int d = st.depth[r];
+      for (int j = 0; j < d; ++j) p.latent[(size_t)root * PL + j] = path[r * PL + j] & 7;
+      for (int j = d; j < PL; ++j) p.latent[(size_t)root * PL + j] = -1;
+    }
+    if (p.latent_len) p.latent_len[root] = p.S > 0 ? st.depth[r] : 0;
+    if (p.pi || p.action) {
+      double v[MZH_A];
+      for (int a = 0; a < MZH_A; ++a) v[a] = (double)vis[a];
+      if (p.temperature > 0.0) {
+        double ex = 1.0 / p.temperature;
+        ex = ex < 5.0 ? ex : 5.0;  // max(1.0, min(5.0, 1/T))
+        ex = ex > 1.0 ? ex : 1.0;
+        for (int a = 0; a < MZH_A; ++a) v[a] = mzh_pow(v[a], ex);
+      }
+      double sum = 0.0;
+      for (int a = 0; a < MZH_A; ++a) sum = sum + v[a];
+      double pi[MZH_A];
+      for (int a = 0; a < MZH_A; ++a) pi[a] = v[a] / sum;
+      if (p.pi)
+        for (int a = 0; a < MZH_A; ++a) p.pi[(size_t)root * MZH_A + a] = pi[a];
+      int act = 0;
+      if (p.deterministic || !p.action_u) {
+        for (int a = 1; a < MZH_A; ++a)
+          if (vis[a] > vis[act]) act = a;
+      } else {
+        double cdf[MZH_A];
+        double acc = 0.0;
+        for (int a = 0; a < MZH_A; ++a) {
+          acc = acc + pi[a];
+          cdf[a] = acc;
+        }
+        const double last = cdf[MZH_A - 1];
+        const double u = p.action_u[root];
+        act = MZH_A - 1;
+        for (int a = 0; a < MZH_A; ++a) {
+          if (cdf[a] / last > u) {
+            act = a;
+            break;
+          }
+        }
+      }
+      if (p.action) p.action[root] = act;
+    }
+  }
+};

@@ -17,8 +17,8 @@ from muzero_hanoi_amd.networks import MuZeroNet  # noqa: E402
 
 MLP = {0: "prologue", 1: "dyn0", 2: "bar+fetch", 3: "dyn2", 4: "bar+fetch", 5: "norm", 6: "rwd0", 7: "bar+fetch",
        8: "rwd2|pred4", 9: "pred4+pred3", 10: "bar+pol2/val2", 11: "bar+heads", 12: "bar"}
-SEARCH = {16: "loop-top", 29: "select:root level", 30: "select:loop", 17: "select:gather", 18: "bar", 19: "gather+bar", 20: "mlp", 21: "store h", 22: "expand+backup",
-          23: "bar"}
+SEARCH = {16: "select:start", 29: "select:root level", 30: "select:loop", 17: "select:gather", 18: "(unused)",
+          19: "bar->mlp", 20: "mlp", 21: "heads", 22: "expand+backup", 23: "bar"}
 
 
 def main():
