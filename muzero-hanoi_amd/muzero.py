@@ -3,7 +3,11 @@
 Same constructor and `training_loop(n_loops, min_replay_size, print_acc)` as the reference, so
 `training_main.py` can construct it unchanged.  What runs where on the MI355X:
   * self-play (`_play_game`): every search is one fused libmzh kernel launch (mcts.MCTS) and the
-    environment step is the reference's (selfplay.play_game);
+    environment step is the reference's (selfplay.play_game); with selfplay="batched" the
+    n_ep_x_loop episodes of a loop play in lockstep -- one search launch and one env-kernel launch
+    per step for all of them (selfplay.BatchedSelfPlay), each episode an agent whose MinMaxStats
+    starts from the MCTS instance's, then the reference's per-episode bookkeeping
+    (selfplay.episode_records) and buffer filter;
   * the replay buffer keeps its transitions on the training device (buffer.Buffer);
   * the update (`_update`, Muzero.py:209-274): the 5-step unrolled loss of the reference -- the
     same torch operations in the same order (represent, prediction/dynamics per unroll step,
@@ -23,14 +27,14 @@ from torch.autograd.graph import increment_version
 from .buffer import Buffer
 from .mcts import MCTS
 from .networks import MuZeroNet
-from .selfplay import play_game
-from .utils import organise_transitions
+from .selfplay import BatchedSelfPlay, episode_records, play_game
+from .utils import adjust_temperature, organise_transitions
 
 
 class Muzero:
     def __init__(self, env, s_space_size, n_action, discount, dirichlet_alpha, n_mcts_simulations, unroll_n_steps,
                  batch_s, TD_return, n_TD_step, lr, buffer_size, priority_replay, device, n_ep_x_loop=1,
-                 n_update_x_loop=1, update_impl="torch"):
+                 n_update_x_loop=1, update_impl="torch", selfplay="sequential"):
         self.dev = device
         self.env = env
         self.n_ep_x_loop = n_ep_x_loop  # episodes collected per training loop
@@ -55,6 +59,11 @@ class Muzero:
         self._graphed = {"torch": None, "graph": GraphedUpdate, "fused": FusedUpdate}[update_impl]
         if self._graphed is not None:
             self._graphed = self._graphed(self)
+        # selfplay (not in the reference's signature): "sequential" = one episode after another as
+        # Muzero._play_game runs them; "batched" = a loop's n_ep_x_loop episodes in lockstep
+        if selfplay not in ("sequential", "batched"):
+            raise ValueError(f"selfplay must be 'sequential' or 'batched', not {selfplay!r}")
+        self.selfplay = selfplay
 
     # ------------------------------------------------------------------ Muzero.py:81-151
     def training_loop(self, n_loops, min_replay_size, print_acc=50):
@@ -63,9 +72,12 @@ class Muzero:
         value_loss, rwd_loss, pi_loss = [], [], []
         for n in range(1, n_loops):
             ep_steps = []
-            for _ in range(self.n_ep_x_loop):
-                steps, states, rwds, actions, pi_probs, returns, priorities = self._play_game(
-                    episode=n * self.n_ep_x_loop, deterministic=False)
+            if self.selfplay == "batched":
+                episodes = self._play_games(self.n_ep_x_loop, episode=n * self.n_ep_x_loop, deterministic=False)
+            else:
+                episodes = (self._play_game(episode=n * self.n_ep_x_loop, deterministic=False)
+                            for _ in range(self.n_ep_x_loop))
+            for steps, states, rwds, actions, pi_probs, returns, priorities in episodes:
                 ep_steps.append(steps)
                 if returns[-1, 0] > 0:  # only successful episodes enter the buffer
                     self.buffer.add(states, rwds, actions, pi_probs, returns, priorities)
@@ -96,6 +108,24 @@ class Muzero:
         return play_game(self.env, self.mcts, self.networks, episode, deterministic, discount=self.discount,
                          TD_return=self.TD_return, n_step=self.n_step, unroll_n_steps=self.unroll_n_steps,
                          n_action=self.n_action)
+
+    def _play_games(self, n_games, episode, deterministic=False):
+        """n_games episodes from env.reset()'s start in lockstep (BatchedSelfPlay): each one an
+        agent whose MinMaxStats starts from this MCTS instance's; afterwards the instance keeps
+        the union (max of the maxima, min of the minima).  Draws come from the global NumPy stream
+        (for n_games = 1 exactly the draws of _play_game).  Returns _play_game's tuple per episode."""
+        env, mm = self.env, self.mcts.min_max_stats
+        sp = BatchedSelfPlay(self.networks, env.discs, env.max_steps, int(self.mcts.n_simulations),
+                             discount=self.discount, dirichlet_alpha=self.mcts.root_dirichlet_alpha,
+                             root_exploration_eps=self.mcts.root_exploration_eps, goal_peg=env.goal[0],
+                             np1_ucb=self.mcts.np1_ucb)
+        res = sp.play([env.init_state_idx] * n_games, temperature=adjust_temperature(episode),
+                      deterministic=deterministic, legacy_rng=True,
+                      minmax=[[mm.maximum, mm.minimum]] * n_games, record_obs=True)
+        fin = res["minmax"].cpu().numpy()
+        mm.maximum, mm.minimum = float(fin[:, 0].max()), float(fin[:, 1].min())
+        return episode_records(res, discount=self.discount, TD_return=self.TD_return, n_step=self.n_step,
+                               unroll_n_steps=self.unroll_n_steps, n_action=self.n_action)
 
     # ------------------------------------------------------------------ Muzero.py:209-274
     def _update(self, states, rwds, actions, pi_probs, returns, priority_w):

@@ -18,6 +18,9 @@ Fixtures (see tests/golden/README.md):
                           final visits / pi / rootQ / action / min-max (MCTS/mcts.py:34-126)
   training_<case>.npz     Buffer sampling + Muzero._update steps: indices, IS weights, losses,
                           new priorities, parameters and Adam moments (Muzero.py:209-274, buffer.py)
+  acting_<case>.npz       acting_ablations.get_results runs (every network output, actions, env
+                          results, MinMaxStats, the returned data, the RNG position after)
+  illegal_<case>.npz      illegal_move_rate_comparison.illegal_move_rate runs (same records)
 """
 import json
 import os
@@ -370,6 +373,118 @@ def gen_episode(name, n, s, max_steps, seed, episode, deterministic, wseed=0, td
     )
 
 
+def _split_calls(calls):
+    """Recorder calls -> one record per run_mcts: (obs, root_pi, pi[S,6], reward[S], value[S])"""
+    runs, cur = [], None
+    for kind, x, a, out in calls:
+        if kind == "i":
+            cur = dict(obs=np.asarray(x, np.float64).reshape(-1), root_pi=np.asarray(out[2], np.float32), pi=[],
+                       reward=[], value=[])
+            runs.append(cur)
+        else:
+            cur["pi"].append(np.asarray(out[2], np.float32))
+            cur["reward"].append(np.float32(out[1]))
+            cur["value"].append(np.float32(out[3]))
+    return runs
+
+
+def _pack_runs(runs):
+    """flatten per-run recorded outputs (the replay network of the tests consumes them in order)"""
+    S = np.array([len(r["pi"]) for r in runs], np.int32)
+    cat = lambda k, shape: (np.concatenate([np.asarray(r[k], np.float32).reshape((-1,) + shape) for r in runs])
+                            if S.sum() else np.zeros((0,) + shape, np.float32))
+    return dict(run_S=S, run_obs=np.array([r["obs"] for r in runs]), run_root_pi=np.array([r["root_pi"] for r in runs]),
+                run_pi=cat("pi", (6,)), run_reward=cat("reward", ()), run_value=cat("value", ()))
+
+
+class _ActingMCTS(TracingMCTS):
+    """records every run_mcts result (action, root Q, MinMaxStats after the call)"""
+
+    def run_mcts(self, state, network, temperature, deterministic):
+        out = super().run_mcts(state, network, temperature, deterministic)
+        self.trace.append((int(out[0]), float(out[2]), self.min_max_stats.maximum, self.min_max_stats.minimum))
+        return out
+
+
+def _traced_env(n, max_steps):
+    """TowersOfHanoi whose step() results are recorded (illegal flags, rewards)"""
+    env = TowersOfHanoi(N=n, max_steps=max_steps)
+    env.trace = []
+    orig = env.step
+
+    def step(a):
+        out = orig(a)
+        env.trace.append((int(a), float(out[1]), int(out[2]), int(out[3])))
+        return out
+
+    env.step = step
+    return env
+
+
+def gen_acting(name, n, budgets, episodes, start, temperature, max_steps, seed, wseed=0):
+    """acting_experiments/acting_ablations.py:72-128 get_results of the reference: ONE MCTS instance
+    for every budget and episode (MinMaxStats carried across all of them), starts from
+    get_starting_state (ES/MS/LS, :49-68) or random_reset (env/hanoi.py:98-109), every network
+    output recorded per run_mcts call."""
+    sys.path.insert(0, os.path.join(REF, "acting_experiments"))
+    import acting_ablations as aa
+
+    net = make_net(n, wseed)
+    rec = Recorder(net)
+    env = _traced_env(n, max_steps)
+    label = aa.get_starting_state(env, start)
+    mcts = _ActingMCTS(discount=0.8, root_dirichlet_alpha=0.25, n_simulations=budgets[0], batch_s=256, device="cpu")
+    mcts.trace = []
+    np.random.seed(seed)
+    data = aa.get_results(env, start, rec, mcts, episodes, budgets, temperature)
+    runs = _split_calls(rec.calls)
+    tr = np.array(mcts.trace, np.float64).reshape(-1, 4)
+    et = np.array(env.trace, np.float64).reshape(-1, 4)
+    np.savez_compressed(
+        os.path.join(HERE, f"acting_{name}.npz"), n=n, budgets=np.array(budgets, np.int32), episodes=episodes,
+        start=-1 if start is None else start, start_label=label, temperature=temperature, max_steps=max_steps,
+        seed=seed, wseed=wseed, init_state_idx=env.init_state_idx, data=np.array(data, np.float64),
+        actions=tr[:, 0].astype(np.int32), root_q=tr[:, 1], mm=tr[:, 2:], env_rwd=et[:, 1],
+        env_done=et[:, 2].astype(np.int32), env_illegal=et[:, 3].astype(np.int32), **_pack_runs(runs),
+        post_rng=np.random.random_sample(4))
+
+
+def gen_illegal(name, n, n_sims, episodes, temperature, fixed_start, max_steps, seed, wseed=0, init_state_idx=0):
+    """illegal_move_rate_comparison.py:27-50 illegal_move_rate of the reference (per-episode rates,
+    their mean and standard error), every network output recorded."""
+    import illegal_move_rate_comparison as imr
+
+    net = make_net(n, wseed)
+    rec = Recorder(net)
+    env = _traced_env(n, max_steps)
+    env.init_state_idx = init_state_idx
+    mcts = _ActingMCTS(discount=0.8, root_dirichlet_alpha=0.25, n_simulations=n_sims, batch_s=1, device="cpu")
+    mcts.trace = []
+    np.random.seed(seed)
+    mean, sem = imr.illegal_move_rate(env, rec, mcts, episodes=episodes, temperature=temperature,
+                                      fixed_start=fixed_start)
+    runs = _split_calls(rec.calls)
+    tr = np.array(mcts.trace, np.float64).reshape(-1, 4)
+    et = np.array(env.trace, np.float64).reshape(-1, 4)
+    np.savez_compressed(
+        os.path.join(HERE, f"illegal_{name}.npz"), n=n, n_sims=n_sims, episodes=episodes, temperature=temperature,
+        fixed_start=int(fixed_start), max_steps=max_steps, seed=seed, wseed=wseed, init_state_idx=init_state_idx,
+        mean=mean, sem=sem, actions=tr[:, 0].astype(np.int32), mm=tr[:, 2:], env_done=et[:, 2].astype(np.int32),
+        env_illegal=et[:, 3].astype(np.int32), **_pack_runs(runs), post_rng=np.random.random_sample(4))
+
+
+ACTING_CASES = [
+    # name, n, budgets, episodes, start, temperature, max_steps, seed
+    ("es_t1", 3, [1, 3, 5], 2, 0, 1.0, 30, 21),
+    ("rand_t05", 3, [2, 4], 3, None, 0.5, 25, 22),
+]
+ILLEGAL_CASES = [
+    # name, n, n_sims, episodes, temperature, fixed_start, max_steps, seed
+    ("rand_t0", 3, 5, 4, 0.0, False, 25, 31),
+    ("fixed_t1", 3, 3, 3, 1.0, True, 20, 32),
+]
+
+
 def gen_checkpoint():
     """A muzero_model.pt in the reference's format (training_main.py:91-103) after one Adam step,
     plus the weights after the reference's own head ablation (acting_ablations.py:29-45)."""
@@ -458,6 +573,16 @@ EPISODE_CASES = [
 
 
 def main():
+    if "--acting-only" in sys.argv:
+        for c in ACTING_CASES:
+            gen_acting(*c)
+        for c in ILLEGAL_CASES:
+            gen_illegal(*c)
+        return
+    for c in ACTING_CASES:
+        gen_acting(*c)
+    for c in ILLEGAL_CASES:
+        gen_illegal(*c)
     for name, n, td, prio, full in TRAINING_CASES:
         gen_training(name, n, td, prio, full=full)
     gen_checkpoint()

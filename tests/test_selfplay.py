@@ -92,7 +92,8 @@ def test_episode_replay_dropin_gpu(name):
 
 @pytest.mark.gpu
 def test_batched_selfplay_vs_oracle(oracle):
-    """B envs in lockstep on the GPU == the same episodes simulated with the oracle (MLP mode)."""
+    """B envs in lockstep on the GPU == the same episodes simulated with the oracle (MLP mode), each
+    env one agent whose MinMaxStats is carried from decision to decision (MCTS/mcts.py:23)."""
     from muzero_hanoi_amd.networks import MuZeroNet
     from muzero_hanoi_amd.selfplay import BatchedSelfPlay
 
@@ -103,9 +104,13 @@ def test_batched_selfplay_vs_oracle(oracle):
 
     flat = flat_weights(net.state_dict())
     starts = np.random.RandomState(1).randint(0, 3 ** n - 1, B)
-    res = BatchedSelfPlay(net, n, max_steps, S).play(starts, temperature=1.0, deterministic=False, seed=seed)
+    mm0 = np.stack([np.linspace(-2.0, 0.0, B), np.linspace(0.5, 3.0, B)], 1)  # agents with history
+    mm0[::3] = (-np.inf, np.inf)  # and fresh ones
+    res = BatchedSelfPlay(net, n, max_steps, S).play(starts, temperature=1.0, deterministic=False, seed=seed,
+                                                     minmax=mm0)
     act = res["action"].cpu().numpy()
     steps = res["steps"].cpu().numpy()
+    mm = mm0.copy()
     # oracle simulation with the same per-step draws
     gen = np.random.default_rng(seed)
     st = np.stack([(starts // 3 ** (n - 1 - d)) % 3 for d in range(n)], 1).astype(np.uint8)
@@ -117,8 +122,10 @@ def test_batched_selfplay_vs_oracle(oracle):
     while alive.any():
         idx = np.nonzero(alive)[0]
         noise, tie, u = mrng.synthetic_draws(len(idx), deterministic=False, alpha=0.25, seed=int(gen.integers(2**31)))
-        o = oracle.search(n, S, obs[idx], flat=flat, support=33, noise=noise, tie_idx=tie, action_u=u, temperature=1.0)
+        o = oracle.search(n, S, obs[idx], flat=flat, support=33, noise=noise, tie_idx=tie, action_u=u, temperature=1.0,
+                          minmax_in=mm[idx])
         assert np.array_equal(o["action"], act[t, idx]), f"step {t}"
+        mm[idx] = np.stack([o["mm_max"], o["mm_min"]], 1)
         for j, b in enumerate(idx):
             code, s2, moved, c2, a2, d, ill = oracle.env_step(st[b], int(o["action"][j]), int(ctr[b]), 1, max_steps)
             st[b], ctr[b] = s2, c2
@@ -129,3 +136,73 @@ def test_batched_selfplay_vs_oracle(oracle):
         t += 1
     assert t == act.shape[0]
     assert np.all(steps == (act >= 0).sum(0))
+    assert np.array_equal(res["minmax"].cpu().numpy(), mm)
+
+
+def _fresh_net(n, seed=0):
+    from muzero_hanoi_amd.networks import MuZeroNet
+
+    torch.manual_seed(seed)
+    return MuZeroNet(3 * n, 6, 0.002, "cpu", TD_return=True)
+
+
+@pytest.mark.gpu
+def test_batched_b1_equals_play_game():
+    """One env through BatchedSelfPlay (global NumPy stream, the agent's MinMaxStats carried in and
+    out) + episode_records == Muzero._play_game through the drop-ins, bit for bit, RNG included."""
+    from muzero_hanoi_amd.env import TowersOfHanoi
+    from muzero_hanoi_amd.mcts import MCTS
+    from muzero_hanoi_amd.selfplay import BatchedSelfPlay, episode_records, play_game
+
+    n, S, max_steps = 3, 10, 40
+    net = _fresh_net(n)
+    env = TowersOfHanoi(N=n, max_steps=max_steps, init_state_idx=4)
+    mcts = MCTS(discount=0.8, root_dirichlet_alpha=0.25, n_simulations=S, batch_s=256, device="cpu")
+    mcts.min_max_stats.maximum, mcts.min_max_stats.minimum = 0.25, -0.5
+    np.random.seed(123)
+    ref = play_game(env, mcts, net, episode=600, deterministic=False, n_step=10)
+    ref_rng = np.random.random_sample(3)
+    np.random.seed(123)
+    res = BatchedSelfPlay(net, n, max_steps, S).play([4], temperature=0.5, legacy_rng=True, minmax=[[0.25, -0.5]],
+                                                     record_obs=True)
+    got = episode_records(res, n_step=10)[0]
+    assert got[0] == ref[0]
+    for a, b in zip(got[1:], ref[1:]):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    assert np.array_equal(np.random.random_sample(3), ref_rng)
+    assert tuple(res["minmax"][0].tolist()) == (mcts.min_max_stats.maximum, mcts.min_max_stats.minimum)
+
+
+@pytest.mark.gpu
+def test_muzero_batched_selfplay():
+    """Muzero(selfplay="batched"): a loop's episodes in one lockstep batch.  With one episode per loop
+    the buffer, the MCTS instance's MinMaxStats and the RNG stream equal the sequential agent's;
+    with several, every episode is recorded with the reference's bookkeeping."""
+    from muzero_hanoi_amd.env import TowersOfHanoi
+    from muzero_hanoi_amd.muzero import Muzero
+
+    def agent(mode, n_ep):
+        torch.manual_seed(3)
+        env = TowersOfHanoi(N=3, max_steps=60)
+        return Muzero(env=env, s_space_size=9, n_action=6, discount=0.8, dirichlet_alpha=0.25, n_mcts_simulations=8,
+                      unroll_n_steps=5, batch_s=16, TD_return=True, n_TD_step=10, lr=0.002, buffer_size=5000,
+                      priority_replay=True, device="cuda", n_ep_x_loop=n_ep, selfplay=mode)
+
+    outs = []
+    for mode in ("sequential", "batched"):
+        mz = agent(mode, 1)
+        np.random.seed(9)
+        mz.training_loop(n_loops=4, min_replay_size=10**9, print_acc=1000)
+        outs.append((len(mz.buffer), mz.buffer.priorities[:len(mz.buffer)].copy(), mz.mcts.min_max_stats.maximum,
+                     mz.mcts.min_max_stats.minimum, np.random.random_sample(2)))
+    assert outs[0][0] == outs[1][0]
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert outs[0][2:4] == outs[1][2:4] and np.array_equal(outs[0][4], outs[1][4])
+    mz = agent("batched", 4)
+    np.random.seed(9)
+    eps = mz._play_games(4, episode=1)
+    assert len(eps) == 4
+    for steps, states, rwds, actions, pi_probs, returns, prio in eps:
+        assert states.shape == (steps, 9) and rwds.shape == (steps, 5) and returns.shape == (steps, 5)
+        assert prio.shape == (steps,) and np.allclose(pi_probs.sum(-1), 1.0)
+        assert np.all(states.sum(1) == 3)  # one-hot 3-disk observations

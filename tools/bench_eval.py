@@ -5,7 +5,8 @@ count from hanoi_solver (env/hanoi_utils.py:4-26), and the illegal-move rate
 (illegal_move_rate_comparison.py:27-50) -- plus the hanoi_solver kernel alone.
 
 Legs:
-  evaluate     selfplay.evaluate on the GPU: every start of a budget in one lockstep batch
+  evaluate     selfplay.evaluate on the GPU: every start of a budget in one lockstep batch, each
+               episode its own agent (MinMaxStats carried over its decisions)
   solver       device hanoi_solver over 2^20 random states (N=7) vs the C restatement on one host
                core (bench.cpu_baseline_solver, bounded sample)
 
@@ -44,15 +45,16 @@ def main():
     net = MuZeroNet(3 * a.disks, 6, 0.002, "cuda", TD_return=True).to("cuda")
     budgets = [int(x) for x in a.budgets.split(",")]
     starts = np.random.default_rng(0).integers(0, 3 ** a.disks - 1, size=a.starts)
-    evaluate(net, a.disks, starts[:64], budgets[:1], max_steps=a.max_steps)  # warm-up
+    evaluate(net, a.disks, budgets[:1], start_idx=starts[:64], max_steps=a.max_steps)  # warm-up
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    data = evaluate(net, a.disks, starts, budgets, max_steps=a.max_steps)
+    out = evaluate(net, a.disks, budgets, start_idx=starts, max_steps=a.max_steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     recs.append({"leg": "evaluate", "metric": "evaluate_seconds", "value": dt, "unit": "s",
                  "episodes": a.starts * len(budgets), "episodes_per_sec": a.starts * len(budgets) / dt,
-                 "results": [{"n_sims": n, "mean_steps_over_optimal": e, "illegal_rate": il} for n, e, il in data],
+                 "results": [{"n_sims": n, "mean_steps_over_optimal": e, "illegal_rate_mean": il, "illegal_rate_sem": se}
+                             for (n, e), (_, il, se) in zip(out["data"], out["illegal"])],
                  "config": {"workload": f"hanoi{a.disks}_maxsteps{a.max_steps}", "starts": a.starts,
                             "budgets": budgets, "network": "random-init MuZeroNet(TD_return=True)"}})
     print(json.dumps(recs[-1]), flush=True)
