@@ -21,6 +21,9 @@ Fixtures (see tests/golden/README.md):
   acting_<case>.npz       acting_ablations.get_results runs (every network output, actions, env
                           results, MinMaxStats, the returned data, the RNG position after)
   illegal_<case>.npz      illegal_move_rate_comparison.illegal_move_rate runs (same records)
+  ucb_np1_vs_np2.npz      child_U under NumPy-2 (the reference's own, here) and NumPy-1 promotion
+  tie_replay.npz          a run_mcts trace with argmax ties beyond the root's first selection
+  random_reset.npz        TowersOfHanoi.random_reset start states from a seeded global stream
 """
 import json
 import os
@@ -473,6 +476,124 @@ def gen_illegal(name, n, n_sims, episodes, temperature, fixed_start, max_steps, 
         env_illegal=et[:, 3].astype(np.int32), **_pack_runs(runs), post_rng=np.random.random_sample(4))
 
 
+def gen_ucb_rules(n_rows=1000, seed=41):
+    """child_U (MCTS/node.py:105-123) under the two NumPy promotion rules.  The reference pins
+    numpy==1.25.2 (requirements.txt:17): np.float32 prior * Python-float w is promoted to float64 and
+    rounded once into the float32 array, fl32(fl64(prior) * w); NumPy >= 2 (NEP 50, this container)
+    keeps float32: fl32(prior * fl32(w)).  Rows are (N_parent, N_child, prior) triples drawn at random;
+    the reference's own child_U (run here, NumPy 2) pins the NumPy-2 column, the NumPy-1 column is the
+    stated rule evaluated explicitly (no NumPy-1 run is possible here: parity unpinned for it)."""
+    import math
+
+    from MCTS.node import Node
+
+    class Cfg:
+        pb_c_base, pb_c_init = 19652, 1.25
+
+    rs = np.random.RandomState(seed)
+    rows = []
+    for _ in range(n_rows):
+        npar = int(rs.randint(1, 400))
+        prior = rs.dirichlet(np.ones(6)).astype(np.float32)
+        parent = Node(prior=None)
+        parent.expand(prior, None, 0.0)
+        parent.N = npar
+        nc = rs.randint(0, npar, 6)
+        for c, k in zip(parent.children, nc):
+            c.N = int(k)
+        u_ref = parent.child_U(Cfg)  # the reference, NumPy 2 semantics
+        for c, k, u2 in zip(parent.children, nc, u_ref):
+            w = (math.log((npar + 19652 + 1) / 19652) + 1.25) * math.sqrt(npar) / (int(k) + 1)
+            np2 = np.float32(np.float32(c.prior) * np.float32(w))
+            np1 = np.float32(np.float64(c.prior) * w)
+            assert np2 == u2
+            rows.append((npar, int(k), float(c.prior), float(np1), float(np2)))
+    a = np.array(rows, np.float64)
+    differ = a[:, 3] != a[:, 4]
+    np.savez_compressed(os.path.join(HERE, "ucb_np1_vs_np2.npz"), n_parent=a[:, 0].astype(np.int32),
+                        n_child=a[:, 1].astype(np.int32), prior=a[:, 2].astype(np.float32),
+                        u_np1=a[:, 3].astype(np.float32), u_np2=a[:, 4].astype(np.float32), differ=differ)
+    return int(differ.sum()), len(rows)
+
+
+def gen_tie_replay(n=3, s=12, n_roots=4, seed=51, wseed=0):
+    """A run_mcts trace that meets argmax ties beyond the root's first selection: the recorded
+    network returns uniform priors, so every freshly expanded node's first selection is a 6-way
+    tie (MCTS/node.py:83-86).  np.random.choice over an argmax set is replaced (in this script)
+    by the LOWEST index -- the resolution the kernels apply to such extra ties -- so the trace is
+    the reference's tree under that resolution; the number of multi-candidate argmax choices per
+    root is recorded (the kernels count all but the root's first as extra_ties)."""
+    net = make_net(n, wseed)
+
+    class UniformRecorder(Recorder):
+        def initial_inference(self, x):
+            h, r, pi, v = self.net.initial_inference(x)
+            out = (h, r, np.full(6, 1.0 / 6.0, np.float32), v)
+            self.calls.append(("i", x.numpy().copy(), -1, out))
+            return out
+
+        def recurrent_inference(self, h, a):
+            h2, r, pi, v = self.net.recurrent_inference(h, a)
+            out = (h2, r, np.full(6, 1.0 / 6.0, np.float32), v)
+            self.calls.append(("r", h.numpy().copy(), int(a.argmax()), out))
+            return out
+
+    orig = np.random.choice
+    ties = []
+
+    def lowest(a, *args, **kw):
+        if "p" in kw or isinstance(a, (int, np.integer)):
+            return orig(a, *args, **kw)
+        ties[-1] += int(len(a) > 1)
+        return int(np.min(a))
+
+    env = TowersOfHanoi(N=n, max_steps=200)
+    rs = np.random.RandomState(seed)
+    roots = [int(i) for i in rs.randint(0, 3 ** n - 1, n_roots)]
+    out = dict(visits=[], rootQ=[], mm=[], pi=[], root_pi=[], rwd=[], value=[], obs=[])
+    np.random.seed(seed)
+    np.random.choice = lowest
+    try:
+        for idx in roots:
+            ties.append(0)
+            mcts = TracingMCTS(discount=0.8, root_dirichlet_alpha=0.0, n_simulations=s, batch_s=1, device="cpu")
+            obs = np.zeros(3 * n)
+            obs[np.arange(n) * 3 + np.array(env.states[idx])] = 1.0
+            rec = UniformRecorder(net)
+            _, pi, q = mcts.run_mcts(obs, rec, 1.0, True)
+            run = _split_calls(rec.calls)[0]
+            out["visits"].append(mcts.last_visits.astype(np.int32))
+            out["rootQ"].append(float(q))
+            out["mm"].append((mcts.min_max_stats.maximum, mcts.min_max_stats.minimum))
+            out["pi"].append(np.array(run["pi"], np.float32))
+            out["root_pi"].append(run["root_pi"])
+            out["rwd"].append(np.array(run["reward"], np.float32))
+            out["value"].append(np.array(run["value"], np.float32))
+            out["obs"].append(obs)
+    finally:
+        np.random.choice = orig
+    np.savez_compressed(os.path.join(HERE, "tie_replay.npz"), n=n, s=s, root_idx=np.array(roots, np.int32),
+                        obs=np.array(out["obs"]), visits=np.array(out["visits"]), rootQ=np.array(out["rootQ"]),
+                        mm=np.array(out["mm"]), root_pi=np.array(out["root_pi"]), pi=np.array(out["pi"]),
+                        rwd=np.array(out["rwd"]), value=np.array(out["value"]), ties=np.array(ties, np.int32))
+    return ties
+
+
+def gen_random_reset(seed=61):
+    """TowersOfHanoi.random_reset (env/hanoi.py:98-109): the start states a seeded global stream
+    gives, for N = 3 and N = 4 and goal pegs 2 / 0, and the stream position after them."""
+    np.random.seed(seed)
+    recs = []
+    for n, goal in ((3, 2), (4, 2), (3, 0)):
+        env = TowersOfHanoi(N=n, max_steps=10, goal_peg=goal)
+        for _ in range(40):
+            env.random_reset()
+            recs.append((n, goal, state_index(env.c_state, n)))
+    a = np.array(recs, np.int32)
+    np.savez_compressed(os.path.join(HERE, "random_reset.npz"), seed=seed, n=a[:, 0], goal_peg=a[:, 1],
+                        state_idx=a[:, 2], post_rng=np.random.random_sample(4))
+
+
 ACTING_CASES = [
     # name, n, budgets, episodes, start, temperature, max_steps, seed
     ("es_t1", 3, [1, 3, 5], 2, 0, 1.0, 30, 21),
@@ -573,12 +694,20 @@ EPISODE_CASES = [
 
 
 def main():
+    if "--corners-only" in sys.argv:
+        print("ucb rows differing", gen_ucb_rules())
+        print("tie counts", gen_tie_replay())
+        gen_random_reset()
+        return
     if "--acting-only" in sys.argv:
         for c in ACTING_CASES:
             gen_acting(*c)
         for c in ILLEGAL_CASES:
             gen_illegal(*c)
         return
+    gen_ucb_rules()
+    gen_tie_replay()
+    gen_random_reset()
     for c in ACTING_CASES:
         gen_acting(*c)
     for c in ILLEGAL_CASES:

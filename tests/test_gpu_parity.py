@@ -210,9 +210,10 @@ def test_search_mlp_end_to_end_vs_oracle(mzh, oracle, case, kernel):
     assert np.array_equal(o["root_q"], ref["rootQ"])
     assert np.array_equal(o["pi"], ref["pi"]) and np.array_equal(o["action"], ref["action"])
     assert np.array_equal(o["sel_steps"], ref["sel_steps"])
-    # and against the reference's own visit counts (torch-CPU network): report agreement
-    agree = (o["visits"] == g["visits"]).all(1).mean()
-    assert agree >= 0.5, agree
+    # and against the reference's own visit counts (torch-CPU network): the measured agreement is
+    # every root of every fixture (tests/test_parity_corners.py pins it on the oracle, 58 / 58)
+    agree = (o["visits"] == g["visits"]).all(1)
+    assert agree.all(), f"{int(agree.sum())} / {len(agree)} histograms equal the reference's"
 
 
 @pytest.mark.parametrize("kernel", KERNELS)

@@ -1,0 +1,243 @@
+"""Parity corners of the search and the env, against fixtures made by
+running the reference here (tests/golden/gen_golden.py):
+
+  ucb_np1_vs_np2.npz  child_U (MCTS/node.py:105-123) under the two NumPy promotion rules.  The
+                      reference pins numpy==1.25.2 (requirements.txt:17), under which the float32
+                      prior times the Python-float w is computed in float64 and rounded once,
+                      fl32(fl64(prior) * w); NumPy >= 2 keeps float32, fl32(prior * fl32(w)).  The
+                      NumPy-2 column is the reference's own child_U; the NumPy-1 column is the rule
+                      evaluated explicitly -- parity unpinned against a NumPy-1 run (no NumPy 1 here).
+                      MZH_FLAG_NP1_UCB / oracle np1_ucb select the NumPy-1 rule.
+  tie_replay.npz      a run_mcts trace with argmax ties beyond the root's first selection (uniform
+                      priors), the reference's np.random.choice replaced by the lowest index in the
+                      generator: the kernels resolve such a tie the same way and count it in
+                      extra_ties (the reference would have drawn from the RNG: the drop-in warns).
+  random_reset.npz    TowersOfHanoi.random_reset (env/hanoi.py:98-109) states from a seeded stream.
+
+Plus the end-to-end agreement of full searches (the oracle's MLP, which the GPU kernels equal bit
+for bit) with the reference's own torch-CPU visit counts, pinned at the measured value.
+"""
+import math
+import warnings
+
+import numpy as np
+import pytest
+
+from conftest import REPLAY_CASES, golden
+from test_oracle_golden import replay_draws, replay_inputs
+
+
+# ------------------------------------------------------------------------------------- NumPy-1 UCB
+def test_ucb_rule_fixture():
+    g = golden("ucb_np1_vs_np2.npz")
+    prior = g["prior"]
+    for npar, nc, p, u1, u2 in zip(g["n_parent"][:2000], g["n_child"][:2000], prior[:2000], g["u_np1"][:2000],
+                                   g["u_np2"][:2000]):
+        w = (math.log((int(npar) + 19652 + 1) / 19652) + 1.25) * math.sqrt(int(npar)) / (int(nc) + 1)
+        assert np.float32(np.float32(p) * np.float32(w)) == u2  # NumPy 2 (NEP 50): float32 arithmetic
+        assert np.float32(np.float64(p) * w) == u1  # NumPy 1.25: float64 product, one rounding
+    frac = float(g["differ"].mean())
+    assert 0.2 < frac < 0.32, frac  # ~26% of evaluations differ in the last bit
+
+
+def _replay_case(oracle, g, np1):
+    n, S = int(g["n"]), int(g["s"])
+    noise, tie, u = replay_draws(g)
+    return oracle.search(n, S, g["obs"], replay=replay_inputs(g), noise=noise, tie_idx=tie, action_u=u,
+                         temperature=float(g["temperature"]), deterministic=bool(g["deterministic"]),
+                         discount=float(g["discount"]), np1_ucb=np1)
+
+
+NP1_CASES = [c for c in REPLAY_CASES if "shared" not in c]
+
+
+def flip_case():
+    """A constructed replay where the two rules pick different children: after the root's first
+    selection (child 5, value -5) the two largest priors are adjacent float32 values that NumPy 2
+    rounds to the same U (a tie: lowest index, counted as an extra tie) while NumPy 1 separates
+    them (child 1 wins).  Found by searching for fl32(p1 * fl32(w)) == fl32(p2 * fl32(w)) with
+    fl32(fl64(p1) * w) != fl32(fl64(p2) * w) at N_parent = 1."""
+    p1 = np.float32(0.460276335477829)
+    p2 = np.nextafter(p1, np.float32(1))
+    S = 4
+    root_pi = np.array([[p1, p2, 0.02, 0.02, 0.02, 0.02]], np.float32)
+    pi = np.full((1, S, 6), 1.0 / 6.0, np.float32)
+    value = np.zeros((1, S), np.float32)
+    value[0, 0] = -5.0
+    obs = np.zeros((1, 9))
+    obs[0, [0, 3, 6]] = 1.0
+    rp = dict(root_pi=root_pi, pi=pi, rwd=np.zeros((1, S), np.float32), value=value)
+    return obs, S, rp, np.array([5], np.int32)
+
+
+def test_np1_rule_flips_a_choice(oracle):
+    obs, S, rp, tie = flip_case()
+    o2 = oracle.search(3, S, obs, replay=rp, tie_idx=tie, temperature=1.0, deterministic=True)
+    o1 = oracle.search(3, S, obs, replay=rp, tie_idx=tie, temperature=1.0, deterministic=True, np1_ucb=True)
+    assert o2["visits"][0, 0] > 0 and o2["visits"][0, 1] == 0  # NumPy 2: the tie resolves to child 0
+    assert o1["visits"][0, 1] > 0 and o1["visits"][0, 0] == 0  # NumPy 1: child 1's larger U wins
+    assert o2["extra_ties"][0] >= 1 and o1["extra_ties"][0] == o2["extra_ties"][0] - 1
+
+
+def test_np2_rule_is_the_reference_here(oracle):
+    """on every replay fixture the NumPy-2 rule reproduces the reference run (this container's NumPy)"""
+    for case in NP1_CASES:
+        g = golden(f"replay_{case}.npz")
+        assert np.array_equal(_replay_case(oracle, g, False)["visits"], g["visits"])
+
+
+# ------------------------------------------------------------------------------------- extra ties
+def _tie_inputs(g):
+    B = g["obs"].shape[0]
+    return B, dict(root_pi=g["root_pi"], pi=g["pi"], rwd=g["rwd"], value=g["value"]), np.zeros(B, np.int32)
+
+
+def test_tie_replay_oracle(oracle):
+    g = golden("tie_replay.npz")
+    B, rp, tie = _tie_inputs(g)
+    o = oracle.search(int(g["n"]), int(g["s"]), g["obs"], replay=rp, tie_idx=tie, temperature=1.0,
+                      deterministic=True)
+    assert np.array_equal(o["visits"], g["visits"]) and np.array_equal(o["rootQ"], g["rootQ"])
+    assert np.array_equal(o["mm_max"], g["mm"][:, 0]) and np.array_equal(o["mm_min"], g["mm"][:, 1])
+    assert np.array_equal(o["extra_ties"], g["ties"] - 1) and (o["extra_ties"] > 0).all()
+
+
+# ------------------------------------------------------------------------------------- random_reset
+def test_random_reset_restatement():
+    from muzero_hanoi_amd.selfplay import _random_start
+
+    g = golden("random_reset.npz")
+    np.random.seed(int(g["seed"]))
+    got = [_random_start(int(n), int(gp)) for n, gp in zip(g["n"], g["goal_peg"])]
+    assert np.array_equal(got, g["state_idx"])
+    assert np.array_equal(np.random.random_sample(4), g["post_rng"])
+
+
+# ------------------------------------------------------------------------------------- end to end
+def _weights(oracle, name):
+    from conftest import GOLDEN
+
+    w, in_dim, sup = oracle.load_weights_npz(f"{GOLDEN}/{name}.npz")
+    return oracle.flat_weights(w), sup
+
+
+def test_end_to_end_agreement_with_reference(oracle):
+    """Full searches with the restated MLP (k-ordered fp32 FMA chains; the GPU kernels are
+    bit-identical to it) against the reference's torch-CPU searches: the MLPs differ in the last
+    bits, so a near-tie could flip a histogram.  Measured: every histogram of
+    every replay fixture agrees (58 / 58 roots) -- pinned, so a change shows up here."""
+    agree = total = 0
+    for case in NP1_CASES:
+        g = golden(f"replay_{case}.npz")
+        n, S, td = int(g["n"]), int(g["s"]), int(g["td"])
+        flat, sup = _weights(oracle, f"weights_N{n}_s{int(g['wseed'])}{'' if td else '_mc'}")
+        noise, tie, u = replay_draws(g)
+        o = oracle.search(n, S, g["obs"], flat=flat, support=sup, noise=noise, tie_idx=tie, action_u=u,
+                          temperature=float(g["temperature"]), deterministic=bool(g["deterministic"]),
+                          discount=float(g["discount"]))
+        same = (o["visits"] == g["visits"]).all(1)
+        agree += int(same.sum())
+        total += len(same)
+    assert (agree, total) == (58, 58)
+
+
+# ------------------------------------------------------------------------------------- GPU
+KERNELS = ["coop", "wave16", "wave"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("case", NP1_CASES)
+def test_np1_replay_gpu(oracle, case, kernel):
+    """MZH_FLAG_NP1_UCB on every kernel == the oracle's NumPy-1 rule, bit for bit"""
+    import torch
+
+    from muzero_hanoi_amd.engine import Engine
+
+    g = golden(f"replay_{case}.npz")
+    n, S = int(g["n"]), int(g["s"])
+    ref = _replay_case(oracle, g, True)
+    noise, tie, u = replay_draws(g)
+    B = g["obs"].shape[0]
+    eng = Engine(n, max(S, 1), B, 33 if int(g["td"]) else 1)
+    tt = lambda a: None if a is None else torch.tensor(np.asarray(a), device="cuda")
+    rp = replay_inputs(g)
+    o = eng.search(S, replay=dict(root_pi=tt(rp["root_pi"]), pi=tt(rp["pi"]), reward=tt(rp["rwd"]),
+                                  value=tt(rp["value"])), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u),
+                   temperature=float(g["temperature"]), deterministic=bool(g["deterministic"]),
+                   discount=float(g["discount"]), np1_ucb=True, kernel=kernel)
+    assert np.array_equal(o["visits"].cpu().numpy(), ref["visits"])
+    assert np.array_equal(o["root_q"].cpu().numpy(), ref["rootQ"])
+    assert np.array_equal(o["minmax"].cpu().numpy()[:, 0], ref["mm_max"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_np1_flip_gpu(oracle, kernel):
+    import torch
+
+    from muzero_hanoi_amd.engine import Engine
+
+    obs, S, rp, tie = flip_case()
+    eng = Engine(3, S, 1, 33)
+    tt = lambda a: torch.tensor(np.asarray(a), device="cuda")
+    for np1 in (False, True):
+        ref = oracle.search(3, S, obs, replay=rp, tie_idx=tie, temperature=1.0, deterministic=True, np1_ucb=np1)
+        o = eng.search(S, replay=dict(root_pi=tt(rp["root_pi"]), pi=tt(rp["pi"]), reward=tt(rp["rwd"]),
+                                      value=tt(rp["value"])), tie_idx=tt(tie), temperature=1.0, deterministic=True,
+                       np1_ucb=np1, kernel=kernel)
+        assert np.array_equal(o["visits"].cpu().numpy(), ref["visits"])
+        assert np.array_equal(o["extra_ties"].cpu().numpy(), ref["extra_ties"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_tie_replay_gpu(kernel):
+    import torch
+
+    from muzero_hanoi_amd.engine import Engine
+
+    g = golden("tie_replay.npz")
+    B, rp, tie = _tie_inputs(g)
+    eng = Engine(int(g["n"]), int(g["s"]), B, 33)
+    tt = lambda a: torch.tensor(np.asarray(a), device="cuda")
+    o = eng.search(int(g["s"]), replay=dict(root_pi=tt(rp["root_pi"]), pi=tt(rp["pi"]), reward=tt(rp["rwd"]),
+                                            value=tt(rp["value"])), tie_idx=tt(tie), temperature=1.0,
+                   deterministic=True, kernel=kernel)
+    assert np.array_equal(o["visits"].cpu().numpy(), g["visits"])
+    assert np.array_equal(o["extra_ties"].cpu().numpy(), g["ties"] - 1)
+
+
+@pytest.mark.gpu
+def test_tie_warning_dropin():
+    """MCTS.run_mcts tells the caller when a search met an extra tie (its RNG stream then differs
+    from the reference's, which would have drawn np.random.choice there)"""
+    from muzero_hanoi_amd.mcts import MCTS, RecordedNetwork
+
+    g = golden("tie_replay.npz")
+    calls = [dict(root_pi=g["root_pi"][b], pi=g["pi"][b], reward=g["rwd"][b], value=g["value"][b])
+             for b in range(g["obs"].shape[0])]
+    net = RecordedNetwork(calls, int(g["n"]))
+    mcts = MCTS(discount=0.8, root_dirichlet_alpha=0.0, n_simulations=int(g["s"]), batch_s=1, device="cpu")
+    np.random.seed(0)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        mcts.run_mcts(g["obs"][0], net, 1.0, True)
+    assert mcts.last_extra_ties == int(g["ties"][0]) - 1
+    assert any(issubclass(x.category, RuntimeWarning) for x in w)
+
+
+@pytest.mark.gpu
+def test_random_reset_dropin():
+    from muzero_hanoi_amd.env import TowersOfHanoi
+    from muzero_hanoi_amd.selfplay import state_index
+
+    g = golden("random_reset.npz")
+    np.random.seed(int(g["seed"]))
+    envs = {}
+    for n, gp, want in zip(g["n"], g["goal_peg"], g["state_idx"]):
+        env = envs.setdefault((int(n), int(gp)), TowersOfHanoi(N=int(n), max_steps=10, goal_peg=int(gp)))
+        obs = env.random_reset()
+        assert state_index(env.c_state) == want
+        assert obs.sum() == int(n) and obs.dtype == np.float64
+    assert np.array_equal(np.random.random_sample(4), g["post_rng"])
