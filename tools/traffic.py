@@ -1,0 +1,88 @@
+"""Summarise one tools/prof.sh run (gpurun_out/prof_<tag>_*): per search kernel instantiation -- the
+fused search (REPLAY = false) and its replay / tree-only instantiation (REPLAY = true) -- the
+rocprofv3 average duration and the per-launch PMC values, HBM bytes corrected as
+MI355X_MICROARCH.md prescribes (FETCH_SIZE x 2 on gfx950, WRITE_SIZE as is; both in KB).
+
+  python tools/traffic.py gpurun_out TAG [--traffic-json profiles/traffic_latest.json WORKLOAD]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def newest(root, pattern):
+    f = sorted(glob.glob(os.path.join(root, pattern)), key=os.path.getmtime)
+    return f[-1] if f else None
+
+
+def kind(name):
+    """search kernels only: 'fused' or 'tree' by the REPLAY template argument"""
+    if "mzh_wave_kernel<" not in name and "mzh_search_kernel<" not in name:
+        return None
+    args = name.split("<", 1)[1].split(">", 1)[0].split(",")
+    return "tree" if args[1].strip() == "true" else "fused"
+
+
+def summarise(root, tag):
+    out = {"fused": {}, "tree": {}}
+    ks = newest(root, f"prof_{tag}_trace/*/*_kernel_stats.csv") or newest(root, f"prof_{tag}_trace/*_kernel_stats.csv")
+    if ks:
+        for r in csv.DictReader(open(ks)):
+            k = kind(r["Name"])
+            if k:
+                out[k].update(kernel=r["Name"], calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]))
+    for p in ("hit", "fetch", "write", "sq"):
+        f = newest(root, f"prof_{tag}_{p}/*/*_counter_collection.csv") or newest(root, f"prof_{tag}_{p}/*_counter_collection.csv")
+        if not f:
+            continue
+        agg = {"fused": collections.defaultdict(lambda: collections.defaultdict(float)),
+               "tree": collections.defaultdict(lambda: collections.defaultdict(float))}
+        for r in csv.DictReader(open(f)):
+            k = kind(r["Kernel_Name"])
+            if k:  # sum the per-XCD / per-SE rows of one dispatch
+                agg[k][r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+        for k in agg:
+            for c, per in agg[k].items():
+                out[k][c] = sum(per.values()) / len(per)  # mean over dispatches
+    for k, d in out.items():
+        if "TCC_HIT_sum" in d:
+            d["l2_hit_rate"] = d["TCC_HIT_sum"] / (d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
+        if "FETCH_SIZE" in d:
+            d["hbm_read_bytes_corrected"] = d["FETCH_SIZE"] * 1024 * 2
+        if "WRITE_SIZE" in d:
+            d["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
+        if "hbm_read_bytes_corrected" in d and "hbm_write_bytes" in d:
+            d["hbm_bytes_per_launch"] = d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"]
+        if "SQ_INSTS_MFMA" in d and "GRBM_GUI_ACTIVE" in d and "avg_ns" in d:
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs; 1024 SIMDs, 32 cycles per 16x16x4 f32 MFMA
+            cyc = d["GRBM_GUI_ACTIVE"] / 8
+            d["clock_ghz"] = cyc / d["avg_ns"]
+            d["mfma_busy_frac"] = d["SQ_INSTS_MFMA"] * 32 / (cyc * 1024)
+    return out
+
+
+def main():
+    root, tag = sys.argv[1], sys.argv[2]
+    out = summarise(root, tag)
+    print(json.dumps(out, indent=1))
+    if "--traffic-json" in sys.argv:
+        i = sys.argv.index("--traffic-json")
+        path, workload = sys.argv[i + 1], sys.argv[i + 2]
+        f, t = out["fused"], out["tree"]
+        json.dump({"workload": workload, "kernel": f.get("kernel"), "avg_ns": f.get("avg_ns"),
+                   "hbm_bytes_per_launch": f.get("hbm_bytes_per_launch"),
+                   "read_bytes_corrected": f.get("hbm_read_bytes_corrected"), "write_bytes": f.get("hbm_write_bytes"),
+                   "l2_hit_rate": f.get("l2_hit_rate"), "mfma_busy_frac": f.get("mfma_busy_frac"),
+                   "clock_ghz": f.get("clock_ghz"),
+                   "tree_kernel": t.get("kernel"), "tree_avg_ns": t.get("avg_ns"),
+                   "tree_hbm_bytes_per_launch": t.get("hbm_bytes_per_launch"),
+                   "source": f"tools/prof.sh TAG={tag} + tools/traffic.py: rocprofv3 --kernel-trace --stats and separate "
+                             "--pmc passes of the bench command; FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, "
+                             "per-dispatch sums, mean over dispatches"}, open(path, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
