@@ -156,8 +156,7 @@ struct PackedLayer {
   int kb = 0, nt = 0;
 };
 
-static PackedLayer pack_layer(std::vector<float>& buf, const float* W, const float* b, int N, int K, int ldw) {
-  PackedLayer L;
+static void pack_weights(std::vector<float>& buf, PackedLayer& L, const float* W, int N, int K, int ldw) {
   L.nt = (N + 15) / 16;
   L.kb = (K + 15) / 16;
   while (buf.size() % 4) buf.push_back(0.0f);
@@ -172,10 +171,17 @@ static PackedLayer pack_layer(std::vector<float>& buf, const float* W, const flo
           const int k = 16 * kb + 4 * j + (lane >> 4);
           dst[(((size_t)nt * L.kb + kb) * 64 + lane) * 4 + j] = (n < N && k < K) ? W[(size_t)n * ldw + k] : 0.0f;
         }
+}
+static void pack_bias(std::vector<float>& buf, PackedLayer& L, const float* b, int N) {
   while (buf.size() % 4) buf.push_back(0.0f);
   L.boff = buf.size();
   buf.resize(buf.size() + (size_t)L.nt * 16, 0.0f);
   for (int n = 0; n < N; ++n) buf[L.boff + n] = b[n];
+}
+static PackedLayer pack_layer(std::vector<float>& buf, const float* W, const float* b, int N, int K, int ldw) {
+  PackedLayer L;
+  pack_weights(buf, L, W, N, K, ldw);
+  pack_bias(buf, L, b, N);
   return L;
 }
 
@@ -258,9 +264,13 @@ extern "C" int mzh_load_weights(mzh_engine* eng, const float* flat, size_t n_flo
   L[3] = pack_layer(buf, dyn2w, dyn2b, H, F, F);
   L[4] = pack_layer(buf, rwd0w, rwd0b, F, H, H);
   L[5] = pack_layer(buf, rwd2w, rwd2b, sup, F, F);
-  L[6] = pack_layer(buf, pol0w, pol0b, F, H, H);
+  // pol0 and val0 weights back to back: the search kernel's prediction chunks take consecutive
+  // tiles of this 32-tile strip and load them as one contiguous run (mzh_mma_store ring refill)
+  pack_weights(buf, L[6], pol0w, F, H, H);
+  pack_weights(buf, L[8], val0w, F, H, H);
+  pack_bias(buf, L[6], pol0b, F);
+  pack_bias(buf, L[8], val0b, F);
   L[7] = pack_layer(buf, pol2w, pol2b, A, F, F);
-  L[8] = pack_layer(buf, val0w, val0b, F, H, H);
   L[9] = pack_layer(buf, val2w, val2b, sup, F, F);
   while (buf.size() % 4) buf.push_back(0.0f);
   const size_t ohoff = buf.size();
@@ -302,6 +312,8 @@ extern "C" int mzh_load_weights(mzh_engine* eng, const float* flat, size_t n_flo
   MzhNet& n = eng->net;
   n.rep0 = mk(L[0]); n.rep2 = mk(L[1]); n.dyn0 = mk(L[2]); n.dyn2 = mk(L[3]); n.rwd0 = mk(L[4]);
   n.rwd2 = mk(L[5]); n.pol0 = mk(L[6]); n.pol2 = mk(L[7]); n.val0 = mk(L[8]); n.val2 = mk(L[9]);
+  if (n.val0.w != n.pol0.w + (size_t)n.pol0.nt * n.pol0.kb * 64)
+    return fail(MZH_ERR_STATE, "pol0/val0 weights not contiguous");
   n.dyn0_onehot = base + ohoff;
   n.support = sup;
   n.in_dim = in;

@@ -391,10 +391,23 @@ __device__ __forceinline__ void mzh_fetch(floatx4* f, float* bv, const MzhChunk&
 // acc = A[rows][0:16KB] . W-tiles ; epilogue (+onehot) + bias (+relu) -> LDS
 // ALL: every tile of the chunk is active (compile-time: no per-tile branches, so the epilogue of
 // one chunk can be scheduled against the MFMAs of the next)
-template <int MT, int NJ, int KB, bool ALL = false>
-__device__ __forceinline__ void mzh_mma_store(const floatx4* f, const float* bv, const MzhChunk& c, const float* A,
-                                              int lda, bool relu, const float* ohv, int lane) {
+// PT > 0: ring refill -- the fragments of the chunk `pc` (PT of them, contiguous from pc->w[0] in
+// slot order, see mzh_ring_contiguous) are loaded into f as this chain frees its slots (slot
+// q*KB + kb after k-block kb; slots this chunk does not use at once), and its PNB biases into bv
+// after the epilogue.  The loads of the chunk after next are spread over this chain's MFMAs instead
+// of issuing as one burst that stalls every wave on the CU's address unit.
+template <int MT, int NJ, int KB, bool ALL = false, int PT = 0, int PNB = 0>
+__device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhChunk& c, const float* A, int lda,
+                                              bool relu, const float* ohv, int lane, const MzhChunk* pc = nullptr) {
+  static_assert(PT <= 16 && PNB <= 4, "ring chunk too large");
   const int r = lane & 15, g = lane >> 4;
+  const float4* pw = PT > 0 ? pc->w[0] : nullptr;
+  auto refill = [&](int slot) {
+    const float4 t = pw[slot * 64 + lane];
+    f[slot] = floatx4{t.x, t.y, t.z, t.w};
+  };
+#pragma unroll
+  for (int slot = NJ * KB; slot < PT; ++slot) refill(slot);
   floatx4 acc[NJ][MT];
 #pragma unroll
   for (int q = 0; q < NJ; ++q)
@@ -428,6 +441,9 @@ __device__ __forceinline__ void mzh_mma_store(const floatx4* f, const float* bv,
         }
       }
     }
+#pragma unroll
+    for (int q = 0; q < NJ; ++q)
+      if (q * KB + kb < PT) refill(q * KB + kb);
   }
 #pragma unroll
   for (int q = 0; q < NJ; ++q) {
@@ -447,6 +463,8 @@ __device__ __forceinline__ void mzh_mma_store(const floatx4* f, const float* bv,
       }
     }
   }
+#pragma unroll
+  for (int q = 0; q < PNB; ++q) bv[q] = pc->bias[q][lane & 15];
 }
 
 // normalize_h_state (networks.py:191-196): 8 lanes per row, 8 elements per lane.
@@ -605,7 +623,7 @@ __device__ __forceinline__ MzhChunk mzh_head_chunk(SM& sm, const MzhNet& net, in
 }
 // waves with a pol2 / val2 tile: all four for 33-bin heads (N2 = 3), waves 0-1 for scalar heads
 template <int N2>
-__device__ __forceinline__ bool mzh_has_head_tile(int wave) { return wave <= N2; }
+__device__ __forceinline__ bool mzh_has_head_tile(int wave) { return N2 == 3 || wave <= N2; }  // compile-time for N2 = 3
 
 // nj consecutive tiles of the prediction hidden layers' 32-tile strip (tiles 0-15: pol0 -> hidP,
 // 16-31: val0 -> hidV; both read the normalised latent), starting at strip tile t0
@@ -687,6 +705,18 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
   constexpr int MT = R / 16;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(wave_in);  // wave-uniform -> chunk descriptors in SGPRs
+  // Weight chunks alternate between the two fragment buffers, each refilled by the chain that
+  // consumes it (ring, mzh_mma_store PT) with the chunk two steps ahead:
+  //   fa: dyn0 -> rwd0 -> P2 -> pol2/val2 -> next dyn0      fb: dyn2 -> rwd2 | P1 -> P3 -> next dyn2
+  // Phase B (after rwd0) balances rwd2 against the prediction hidden layers: waves w < N2 run one
+  // rwd2 tile (K = 256, 4 units) + N2 + 4 prediction tiles (K = 64, 1 unit each), the others N2 + 8
+  // prediction tiles -- 8 + N2 units per wave.
+  const bool r2 = wave < N2;
+  const int P1 = r2 ? wave * (N2 + 4) : N2 * (N2 + 4) + (wave - N2) * (N2 + 8);
+  const int P2 = P1 + (r2 ? 0 : 4), P3 = P2 + 4;
+  const bool ht = mzh_has_head_tile<N2>(wave);
+  const MzhChunk c_rwd0 = mzh_chunk(net.rwd0, wave * 4, 4, sm.hidR, MZH_LD256);
+  const MzhChunk c_p2 = mzh_pred_tiles<R>(sm, net, P2, 4);
   MZH_STAMP_DECL
   {
     // one-hot columns of the dynamics first layer for this lane's rows (k = 64 + action)
@@ -700,53 +730,64 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
         for (int i = 0; i < 4; ++i)
           oh[(q * MT + m) * 4 + i] = onehot[sm.act[m * 16 + g * 4 + i] * MZH_F + (wave * 4 + q) * 16 + r];
     MZH_STAMP(0);
-    mzh_mma_store<MT, 4, 4, true>(fa, ba, mzh_chunk(net.dyn0, wave * 4, 4, sm.hidP, MZH_LD256), sm.x, MZH_LD64, true, oh,
-                            lane);  // dyn0 + one-hot + bias, relu
+    mzh_mma_store<MT, 4, 4, true, 16, 4>(fa, ba, mzh_chunk(net.dyn0, wave * 4, 4, sm.hidP, MZH_LD256), sm.x, MZH_LD64,
+                                         true, oh, lane, &c_rwd0);  // dyn0 + one-hot + bias, relu
   }
   MZH_STAMP(1);
   bar();
-  mzh_fetch<4, 4, true>(fa, ba, mzh_chunk(net.rwd0, wave * 4, 4, sm.hidR, MZH_LD256), lane);
   MZH_STAMP(2);
-  mzh_mma_store<MT, 1, 16, true>(fb, bb, mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64), sm.hidP, MZH_LD256, false,
-                                 nullptr, lane);  // dyn2 -> h'
+  {
+    const MzhChunk c_b = r2 ? mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP) : mzh_pred_tiles<R>(sm, net, P1, 4);
+    mzh_mma_store<MT, 1, 16, true, 16, 4>(fb, bb, mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64), sm.hidP, MZH_LD256,
+                                          false, nullptr, lane, &c_b);  // dyn2 -> h'
+  }
   MZH_STAMP(3);
   bar();
-  // Phase B (after rwd0) balances rwd2 against the prediction hidden layers: waves w < N2 run one
-  // rwd2 tile (K = 256, 4 units) + N2 + 4 prediction tiles (K = 64, 1 unit each), the others N2 + 8
-  // prediction tiles -- 8 + N2 units per wave.
-  const bool r2 = wave < N2;
-  const int P1 = r2 ? wave * (N2 + 4) : N2 * (N2 + 4) + (wave - N2) * (N2 + 8);
-  const int P2 = P1 + (r2 ? 0 : 4), P3 = P2 + 4;
-  if (r2)
-    mzh_fetch<1, 16, true>(fb, bb, mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP), lane);
-  else
-    mzh_fetch<4, 4, true>(fb, bb, mzh_pred_tiles<R>(sm, net, P1, 4), lane);
   MZH_STAMP(4);
   mzh_normalize_par<R>(sm.hraw, sm.x, tid);
   MZH_STAMP(5);
-  mzh_mma_store<MT, 4, 4, true>(fa, ba, mzh_chunk(net.rwd0, wave * 4, 4, sm.hidR, MZH_LD256), sm.hraw, MZH_LD64, true,
-                          nullptr, lane);  // rwd0 on h' (networks.py:132)
+  mzh_mma_store<MT, 4, 4, true, 16, 4>(fa, ba, c_rwd0, sm.hraw, MZH_LD64, true, nullptr, lane,
+                                       &c_p2);  // rwd0 on h' (networks.py:132)
   MZH_STAMP(6);
   bar();
-  mzh_fetch<4, 4, true>(fa, ba, mzh_pred_tiles<R>(sm, net, P2, 4), lane);
   MZH_STAMP(7);
-  if (r2)
-    mzh_mma_store<MT, 1, 16, true>(fb, bb, mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP), sm.hidR, MZH_LD256, false,
-                                   nullptr, lane);  // rwd2 -> reward logits
-  else
-    mzh_mma_store<MT, 4, 4, true>(fb, bb, mzh_pred_tiles<R>(sm, net, P1, 4), sm.x, MZH_LD64, true, nullptr, lane);
-  mzh_fetch<N2, 4, true>(fb, bb, mzh_pred_tiles<R>(sm, net, P3, N2), lane);
-  MZH_STAMP(8);
-  mzh_mma_store<MT, 4, 4, true>(fa, ba, mzh_pred_tiles<R>(sm, net, P2, 4), sm.x, MZH_LD64, true, nullptr, lane);
-  const bool ht = mzh_has_head_tile<N2>(wave);
-  if (ht) mzh_fetch<1, 16, true>(fa, ba, mzh_head_chunk<R>(sm, net, wave), lane);
-  mzh_mma_store<MT, N2, 4, true>(fb, bb, mzh_pred_tiles<R>(sm, net, P3, N2), sm.x, MZH_LD64, true, nullptr, lane);
+  {
+    const MzhChunk c_p3 = mzh_pred_tiles<R>(sm, net, P3, N2);
+    if (r2)
+      mzh_mma_store<MT, 1, 16, true, 4 * N2, N2>(fb, bb, mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP), sm.hidR,
+                                                 MZH_LD256, false, nullptr, lane, &c_p3);  // rwd2 -> reward logits
+    else
+      mzh_mma_store<MT, 4, 4, true, 4 * N2, N2>(fb, bb, mzh_pred_tiles<R>(sm, net, P1, 4), sm.x, MZH_LD64, true,
+                                                nullptr, lane, &c_p3);
+    MZH_STAMP(8);
+    if (ht) {
+      const MzhChunk c_h = mzh_head_chunk<R>(sm, net, wave);
+      mzh_mma_store<MT, 4, 4, true, 16, 1>(fa, ba, c_p2, sm.x, MZH_LD64, true, nullptr, lane, &c_h);
+    } else {
+      mzh_mma_store<MT, 4, 4, true>(fa, ba, c_p2, sm.x, MZH_LD64, true, nullptr, lane);
+    }
+    if (NEXT) {
+      const MzhChunk c_n2 = mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64);
+      mzh_mma_store<MT, N2, 4, true, 16, 1>(fb, bb, c_p3, sm.x, MZH_LD64, true, nullptr, lane, &c_n2);
+    } else {
+      mzh_mma_store<MT, N2, 4, true>(fb, bb, c_p3, sm.x, MZH_LD64, true, nullptr, lane);
+    }
+  }
   MZH_STAMP(9);
   bar();
-  if (ht)
-    mzh_mma_store<MT, 1, 16, true>(fa, ba, mzh_head_chunk<R>(sm, net, wave), wave == 0 ? sm.hidP : sm.hidV, MZH_LD256,
-                                   false, nullptr, lane);  // pol2 / val2
-  if (NEXT) mzh_mlp_fetch12<R>(sm, net, wave, lane, fa, ba, fb, bb);  // next step's first chunks
+  {
+    const MzhChunk c_n1 = mzh_chunk(net.dyn0, wave * 4, 4, sm.hidP, MZH_LD256);
+    if (ht) {
+      const MzhChunk c_h = mzh_head_chunk<R>(sm, net, wave);
+      float* hin = wave == 0 ? sm.hidP : sm.hidV;
+      if (NEXT)
+        mzh_mma_store<MT, 1, 16, true, 16, 4>(fa, ba, c_h, hin, MZH_LD256, false, nullptr, lane, &c_n1);  // pol2 / val2
+      else
+        mzh_mma_store<MT, 1, 16, true>(fa, ba, c_h, hin, MZH_LD256, false, nullptr, lane);
+    } else if (NEXT) {
+      mzh_fetch<4, 4, true>(fa, ba, c_n1, lane);  // next step's dyn0 chunk
+    }
+  }
   MZH_STAMP(10);
   bar();
   if (HEADS) {
