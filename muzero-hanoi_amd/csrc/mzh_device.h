@@ -228,13 +228,19 @@ struct MzhNet {
 };
 
 // ------------------------------------------------------------------------------------------
-// LDS layout of the MLP block for R roots (R = 16 * MT).  Row strides are 2 (mod 32) dwords so
-// the A-fragment ds_read_b32 pattern (row = lane&15, k = 4t + (lane>>4)) is conflict-free.
+// LDS layout of the MLP block for R roots (R = 16 * MT).  Buffers read as an MFMA A operand (x,
+// hraw, hid*) hold each row's units in *k-block order*: inside every 16-unit block, position
+// 4g + j holds unit 4j + g (mzh_kpos, an involution), so the lane (row r, k-group g) of a
+// 16x16x4 chain finds its four k-steps' operands of one k-block as one aligned float4: one
+// ds_read_b128 per row tile and k-block (one-wave-per-SIMD LDS reads run at full rate only in
+// the 128-bit form).  Row strides 4 (mod 64) dwords: at most 2-way bank sharing for those reads,
+// conflict-free ds_write_b32 of the C fragments.  Logit buffers keep natural order.
 // ------------------------------------------------------------------------------------------
-#define MZH_LD64 66
-#define MZH_LD256 258
+__device__ __forceinline__ int mzh_kpos(int k) { return (k & ~15) | ((k & 3) << 2) | ((k >> 2) & 3); }
+#define MZH_LD64 68
+#define MZH_LD256 260
 #define MZH_LDPOL 16
-#define MZH_LDSUP 48
+#define MZH_LDSUP 40
 
 template <int R>
 struct MlpSmem {
@@ -301,12 +307,12 @@ __device__ __forceinline__ void mzh_run_jobs(const MzhJob* jobs, int KB, const f
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int k = kb * 16 + j * 4 + g;
+      const int kp = kb * 16 + g * 4 + j;  // position of k = 16kb + 4j + g (k-block order)
 #pragma unroll
       for (int q = 0; q < NJ; ++q) {
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
-          float a = jobs[q].A[(m * 16 + r) * jobs[q].lda + k];
+          float a = jobs[q].A[(m * 16 + r) * jobs[q].lda + kp];
           acc[q][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bc[q][j], acc[q][m], 0, 0, 0);
         }
       }
@@ -328,7 +334,7 @@ __device__ __forceinline__ void mzh_run_jobs(const MzhJob* jobs, int KB, const f
         if (onehot) v = v + onehot[act[row] * MZH_F + col];
         v = v + bias;
         if (jobs[q].relu) v = v > 0.0f ? v : 0.0f;
-        jobs[q].out[row * jobs[q].ldo + col] = v;
+        jobs[q].out[row * jobs[q].ldo + mzh_kpos(col)] = v;  // outputs feed the next layer's A
       }
     }
   }
@@ -351,12 +357,14 @@ struct MzhChunk {
   float* out[4];         // LDS output base per tile (a chunk may span two layers sharing A)
   int col0[4];
   int ldo, nj;           // nj: active tiles (wave-uniform), <= NJ
+  bool perm;             // output is an A operand of a later layer: k-block order (mzh_kpos)
 };
 
 __device__ __forceinline__ MzhChunk mzh_chunk(const MzhLayer& L, int nt0, int nj, float* out, int ldo) {
   MzhChunk c;
   c.ldo = ldo;
   c.nj = nj;
+  c.perm = ldo >= MZH_LD64;  // hidden / latent buffers (logit buffers have narrower strides)
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int nt = nt0 + (q < nj ? q : 0);
@@ -416,18 +424,16 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
   // A operands double-buffered one k-block ahead: block kb + 1's LDS reads are issued before block
   // kb's MFMAs (pinned by the scheduling barrier), so a K = 256 chain does not wait on LDS latency
   // between its MFMAs
-  float a[2][4][MT];
+  floatx4 a[2][MT];  // [buffer][row tile]: k-steps j = 0..3 of one k-block (A in k-block order)
+  const float* arow = A + r * lda + 4 * g;
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int m = 0; m < MT; ++m) a[0][j][m] = A[(m * 16 + r) * lda + j * 4 + g];
+  for (int m = 0; m < MT; ++m) a[0][m] = *reinterpret_cast<const floatx4*>(arow + m * 16 * lda);
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
     if (kb + 1 < KB) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int m = 0; m < MT; ++m) a[(kb + 1) & 1][j][m] = A[(m * 16 + r) * lda + (kb + 1) * 16 + j * 4 + g];
+      for (int m = 0; m < MT; ++m)
+        a[(kb + 1) & 1][m] = *reinterpret_cast<const floatx4*>(arow + m * 16 * lda + (kb + 1) * 16);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -437,7 +443,7 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
         if (ALL || q < c.nj) {
 #pragma unroll
           for (int m = 0; m < MT; ++m)
-            acc[q][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kb & 1][j][m], f[q * KB + kb][j], acc[q][m], 0, 0, 0);
+            acc[q][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kb & 1][m][j], f[q * KB + kb][j], acc[q][m], 0, 0, 0);
         }
       }
     }
@@ -447,8 +453,9 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
   }
 #pragma unroll
   for (int q = 0; q < NJ; ++q) {
-    if (ALL || q < c.nj) {
-      const int col = c.col0[q] + r;
+    // output column col0 + r; stored at its k-block-order position for the next layer's A
+    const int pos = c.col0[q] + (c.perm ? 4 * (r & 3) + (r >> 2) : r);
+    if ((ALL || q < c.nj) && pos < c.ldo) {  // (logit padding columns past the row stride dropped)
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
 #pragma unroll
@@ -458,7 +465,7 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
           if (ohv) v = v + ohv[(q * MT + m) * 4 + i];  // one-hot action column (k = 64 + a)
           v = v + bv[q];
           if (relu) v = v > 0.0f ? v : 0.0f;
-          c.out[q][row * c.ldo + col] = v;
+          c.out[q][row * c.ldo + pos] = v;
         }
       }
     }
@@ -632,6 +639,7 @@ __device__ __forceinline__ MzhChunk mzh_pred_tiles(SM& sm, const MzhNet& net, in
   MzhChunk c;
   c.ldo = MZH_LD256;
   c.nj = nj;
+  c.perm = true;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int t = t0 + (q < nj ? q : 0);

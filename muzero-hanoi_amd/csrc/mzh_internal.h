@@ -54,7 +54,7 @@ __device__ __forceinline__ void mzh_store_outputs(MlpSmem<R>& sm, const MzhInfer
   const int tid = threadIdx.x;
   for (int i = tid; i < R * MZH_H; i += MZH_THREADS) {
     const int r = i >> 6, k = i & 63;
-    if (r < nvalid) p.h[(size_t)(row0 + r) * MZH_H + k] = sm.x[r * MZH_LD64 + k];
+    if (r < nvalid) p.h[(size_t)(row0 + r) * MZH_H + k] = sm.x[r * MZH_LD64 + mzh_kpos(k)];
   }
   for (int i = tid; i < R * 8; i += MZH_THREADS) {
     const int r = i >> 3, c = i & 7;

@@ -79,7 +79,7 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
   if (!REPLAY) {
     for (int i = tid; i < R * p.kin; i += MZH_THREADS) {
       const int r = i / p.kin, k = i - r * p.kin;
-      sm.x[r * MZH_LD64 + k] = (r < nvalid && k < p.in_dim) ? p.obs[(size_t)(root0 + r) * p.in_dim + k] : 0.0f;
+      sm.x[r * MZH_LD64 + mzh_kpos(k)] = (r < nvalid && k < p.in_dim) ? p.obs[(size_t)(root0 + r) * p.in_dim + k] : 0.0f;
     }
     __syncthreads();
     mzh_mlp_initial<R>(sm, net, wave, lane);
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_initial_kernel(MzhNet net,
   const int nvalid = min(R, p.B - row0);
   for (int i = tid; i < R * p.kin; i += MZH_THREADS) {
     const int r = i / p.kin, k = i - r * p.kin;
-    sm.x[r * MZH_LD64 + k] = (r < nvalid && k < p.in_dim) ? p.x[(size_t)(row0 + r) * p.in_dim + k] : 0.0f;
+    sm.x[r * MZH_LD64 + mzh_kpos(k)] = (r < nvalid && k < p.in_dim) ? p.x[(size_t)(row0 + r) * p.in_dim + k] : 0.0f;
   }
   __syncthreads();
   mzh_mlp_initial<R>(sm, net, wave, lane);
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_recurrent_kernel(MzhNet ne
   const int nvalid = min(R, p.B - row0);
   for (int i = tid; i < R * MZH_H; i += MZH_THREADS) {
     const int r = i >> 6, k = i & 63;
-    sm.x[r * MZH_LD64 + k] = r < nvalid ? p.x[(size_t)(row0 + r) * MZH_H + k] : 0.0f;
+    sm.x[r * MZH_LD64 + mzh_kpos(k)] = r < nvalid ? p.x[(size_t)(row0 + r) * MZH_H + k] : 0.0f;
   }
   if (tid < R) sm.act[tid] = tid < nvalid ? p.action[row0 + tid] : 0;
   __syncthreads();
