@@ -138,6 +138,16 @@ __device__ __forceinline__ float mzh_sum8(float v) {
   return v;
 }
 
+// the value of the one lane of an aligned 8-lane group with `sel` set, on every lane of the group
+// (an OR over the DPP tree: three VALU steps instead of a ds_bpermute round trip)
+__device__ __forceinline__ int mzh_group_take(int v, bool sel) {
+  int x = sel ? v : 0;
+  x |= __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);
+  x |= __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);
+  x |= __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false);
+  return x;
+}
+
 __device__ __forceinline__ double mzh_dpp_d(double v, int ctrl_sel) {
   const long long b = __double_as_longlong(v);
   const int lo = (int)(b & 0xFFFFFFFFll), hi = (int)(b >> 32);
@@ -357,14 +367,12 @@ struct MzhChunk {
   float* out[4];         // LDS output base per tile (a chunk may span two layers sharing A)
   int col0[4];
   int ldo, nj;           // nj: active tiles (wave-uniform), <= NJ
-  bool perm;             // output is an A operand of a later layer: k-block order (mzh_kpos)
 };
 
 __device__ __forceinline__ MzhChunk mzh_chunk(const MzhLayer& L, int nt0, int nj, float* out, int ldo) {
   MzhChunk c;
   c.ldo = ldo;
   c.nj = nj;
-  c.perm = ldo >= MZH_LD64;  // hidden / latent buffers (logit buffers have narrower strides)
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int nt = nt0 + (q < nj ? q : 0);
@@ -397,16 +405,22 @@ __device__ __forceinline__ void mzh_fetch(floatx4* f, float* bv, const MzhChunk&
 }
 
 // acc = A[rows][0:16KB] . W-tiles ; epilogue (+onehot) + bias (+relu) -> LDS
-// ALL: every tile of the chunk is active (compile-time: no per-tile branches, so the epilogue of
-// one chunk can be scheduled against the MFMAs of the next)
+// ALL: every tile of the chunk is active (compile-time: no per-tile branches).
+// NAT: the output is a logit buffer -- natural column order, padding columns past the row stride
+// dropped; otherwise the output feeds a later layer's A operand and is stored in k-block order.
+// oht / act (dynamics layer 1): + the one-hot action column oht[act[row] * 256 + col] (k = 64 + a),
+// gathered after the first k-block's A reads so the chain does not wait for it.
 // PT > 0: ring refill -- the fragments of the chunk `pc` (PT of them, contiguous from pc->w[0] in
-// slot order, see mzh_ring_contiguous) are loaded into f as this chain frees its slots (slot
-// q*KB + kb after k-block kb; slots this chunk does not use at once), and its PNB biases into bv
-// after the epilogue.  The loads of the chunk after next are spread over this chain's MFMAs instead
-// of issuing as one burst that stalls every wave on the CU's address unit.
-template <int MT, int NJ, int KB, bool ALL = false, int PT = 0, int PNB = 0>
+// slot order) are loaded into f as this chain frees its slots (slot q*KB + kb after k-block kb;
+// slots this chunk does not use at once), and its PNB biases into bv after the epilogue.  The
+// loads of the chunk after next are spread over this chain's MFMAs instead of issuing as one burst
+// that stalls every wave on the CU's address unit.
+// The last k-block runs tile-major, each tile's epilogue right behind its last MFMA, so the
+// stores of tile q overlap the MFMAs of tiles q+1.. instead of trailing the chain.
+template <int MT, int NJ, int KB, bool ALL = false, int PT = 0, int PNB = 0, bool NAT = false>
 __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhChunk& c, const float* A, int lda,
-                                              bool relu, const float* ohv, int lane, const MzhChunk* pc = nullptr) {
+                                              bool relu, const float* oht, const int* act, int lane,
+                                              const MzhChunk* pc = nullptr) {
   static_assert(PT <= 16 && PNB <= 4, "ring chunk too large");
   const int r = lane & 15, g = lane >> 4;
   const float4* pw = PT > 0 ? pc->w[0] : nullptr;
@@ -428,6 +442,36 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
   const float* arow = A + r * lda + 4 * g;
 #pragma unroll
   for (int m = 0; m < MT; ++m) a[0][m] = *reinterpret_cast<const floatx4*>(arow + m * 16 * lda);
+  float oh[NJ * MT * 4];
+  if (oht) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float* ohrow = oht + act[m * 16 + g * 4 + i] * MZH_F + r;
+#pragma unroll
+        for (int q = 0; q < NJ; ++q) oh[(q * MT + m) * 4 + i] = ohrow[c.col0[q]];
+      }
+  }
+  auto epilogue = [&](int q) {
+    // output column col0 + r; a hidden / latent unit is stored at its k-block-order position
+    const int pos = c.col0[q] + (NAT ? r : 4 * (r & 3) + (r >> 2));
+    if ((ALL || q < c.nj) && (!NAT || pos < c.ldo)) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m * 16 + g * 4 + i;
+          float v = acc[q][m][i];
+          if (oht) v = v + oh[(q * MT + m) * 4 + i];
+          v = v + bv[q];
+          if (relu) v = v > 0.0f ? v : 0.0f;
+          c.out[q][row * c.ldo + pos] = v;
+        }
+      }
+    }
+  };
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
     if (kb + 1 < KB) {
@@ -436,37 +480,33 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
         a[(kb + 1) & 1][m] = *reinterpret_cast<const floatx4*>(arow + m * 16 * lda + (kb + 1) * 16);
     }
     __builtin_amdgcn_sched_barrier(0);
+    if (kb + 1 < KB) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int q = 0; q < NJ; ++q) {
+          if (ALL || q < c.nj) {
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+              acc[q][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kb & 1][m][j], f[q * KB + kb][j], acc[q][m], 0, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < NJ; ++q)
+        if (q * KB + kb < PT) refill(q * KB + kb);
+    } else {  // last k-block: tile-major, epilogue behind each tile
 #pragma unroll
       for (int q = 0; q < NJ; ++q) {
         if (ALL || q < c.nj) {
 #pragma unroll
-          for (int m = 0; m < MT; ++m)
-            acc[q][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kb & 1][m][j], f[q * KB + kb][j], acc[q][m], 0, 0, 0);
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+              acc[q][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kb & 1][m][j], f[q * KB + kb][j], acc[q][m], 0, 0, 0);
         }
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < NJ; ++q)
-      if (q * KB + kb < PT) refill(q * KB + kb);
-  }
-#pragma unroll
-  for (int q = 0; q < NJ; ++q) {
-    // output column col0 + r; stored at its k-block-order position for the next layer's A
-    const int pos = c.col0[q] + (c.perm ? 4 * (r & 3) + (r >> 2) : r);
-    if ((ALL || q < c.nj) && pos < c.ldo) {  // (logit padding columns past the row stride dropped)
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = m * 16 + g * 4 + i;
-          float v = acc[q][m][i];
-          if (ohv) v = v + ohv[(q * MT + m) * 4 + i];  // one-hot action column (k = 64 + a)
-          v = v + bv[q];
-          if (relu) v = v > 0.0f ? v : 0.0f;
-          c.out[q][row * c.ldo + pos] = v;
-        }
+        if (q * KB + kb < PT) refill(q * KB + kb);
+        epilogue(q);
       }
     }
   }
@@ -639,7 +679,6 @@ __device__ __forceinline__ MzhChunk mzh_pred_tiles(SM& sm, const MzhNet& net, in
   MzhChunk c;
   c.ldo = MZH_LD256;
   c.nj = nj;
-  c.perm = true;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int t = t0 + (q < nj ? q : 0);
@@ -680,11 +719,12 @@ __device__ void mzh_mlp_initial(SM& sm, const MzhNet& net, int wave_in, int lane
   bar();
   mzh_normalize_par<R>(sm.hraw, sm.x, tid);
   bar();
-  mzh_mma_store<MT, 4, 4, true>(fa, ba, c5, sm.x, MZH_LD64, true, nullptr, lane);
+  mzh_mma_store<MT, 4, 4, true>(fa, ba, c5, sm.x, MZH_LD64, true, nullptr, nullptr, lane);
   mzh_fetch<1, 16>(fa, ba, c7, lane);
-  mzh_mma_store<MT, 4, 4, true>(fb, bb, c6, sm.x, MZH_LD64, true, nullptr, lane);
+  mzh_mma_store<MT, 4, 4, true>(fb, bb, c6, sm.x, MZH_LD64, true, nullptr, nullptr, lane);
   bar();
-  mzh_mma_store<MT, 1, 16>(fa, ba, c7, c7.out[0] == sm.lpol ? sm.hidP : sm.hidV, MZH_LD256, false, nullptr, lane);
+  mzh_mma_store<MT, 1, 16, false, 0, 0, true>(fa, ba, c7, c7.out[0] == sm.lpol ? sm.hidP : sm.hidV, MZH_LD256, false,
+                                            nullptr, nullptr, lane);
   bar();
   mzh_heads_par<R>(sm, net.support, false, tid);
   bar();
@@ -726,35 +766,23 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
   const MzhChunk c_rwd0 = mzh_chunk(net.rwd0, wave * 4, 4, sm.hidR, MZH_LD256);
   const MzhChunk c_p2 = mzh_pred_tiles<R>(sm, net, P2, 4);
   MZH_STAMP_DECL
-  {
-    // one-hot columns of the dynamics first layer for this lane's rows (k = 64 + action)
-    float oh[4 * MT * 4];
-    const int r = lane & 15, g = lane >> 4;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          oh[(q * MT + m) * 4 + i] = onehot[sm.act[m * 16 + g * 4 + i] * MZH_F + (wave * 4 + q) * 16 + r];
-    MZH_STAMP(0);
-    mzh_mma_store<MT, 4, 4, true, 16, 4>(fa, ba, mzh_chunk(net.dyn0, wave * 4, 4, sm.hidP, MZH_LD256), sm.x, MZH_LD64,
-                                         true, oh, lane, &c_rwd0);  // dyn0 + one-hot + bias, relu
-  }
+  MZH_STAMP(0);
+  mzh_mma_store<MT, 4, 4, true, 16, 4>(fa, ba, mzh_chunk(net.dyn0, wave * 4, 4, sm.hidP, MZH_LD256), sm.x, MZH_LD64,
+                                       true, onehot, sm.act, lane, &c_rwd0);  // dyn0 + one-hot + bias, relu
   MZH_STAMP(1);
   bar();
   MZH_STAMP(2);
   {
     const MzhChunk c_b = r2 ? mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP) : mzh_pred_tiles<R>(sm, net, P1, 4);
     mzh_mma_store<MT, 1, 16, true, 16, 4>(fb, bb, mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64), sm.hidP, MZH_LD256,
-                                          false, nullptr, lane, &c_b);  // dyn2 -> h'
+                                          false, nullptr, nullptr, lane, &c_b);  // dyn2 -> h'
   }
   MZH_STAMP(3);
   bar();
   MZH_STAMP(4);
   mzh_normalize_par<R>(sm.hraw, sm.x, tid);
   MZH_STAMP(5);
-  mzh_mma_store<MT, 4, 4, true, 16, 4>(fa, ba, c_rwd0, sm.hraw, MZH_LD64, true, nullptr, lane,
+  mzh_mma_store<MT, 4, 4, true, 16, 4>(fa, ba, c_rwd0, sm.hraw, MZH_LD64, true, nullptr, nullptr, lane,
                                        &c_p2);  // rwd0 on h' (networks.py:132)
   MZH_STAMP(6);
   bar();
@@ -762,23 +790,24 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
   {
     const MzhChunk c_p3 = mzh_pred_tiles<R>(sm, net, P3, N2);
     if (r2)
-      mzh_mma_store<MT, 1, 16, true, 4 * N2, N2>(fb, bb, mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP), sm.hidR,
-                                                 MZH_LD256, false, nullptr, lane, &c_p3);  // rwd2 -> reward logits
+      mzh_mma_store<MT, 1, 16, true, 4 * N2, N2, true>(fb, bb, mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP),
+                                                       sm.hidR, MZH_LD256, false, nullptr, nullptr, lane,
+                                                       &c_p3);  // rwd2 -> reward logits
     else
       mzh_mma_store<MT, 4, 4, true, 4 * N2, N2>(fb, bb, mzh_pred_tiles<R>(sm, net, P1, 4), sm.x, MZH_LD64, true,
-                                                nullptr, lane, &c_p3);
+                                                nullptr, nullptr, lane, &c_p3);
     MZH_STAMP(8);
     if (ht) {
       const MzhChunk c_h = mzh_head_chunk<R>(sm, net, wave);
-      mzh_mma_store<MT, 4, 4, true, 16, 1>(fa, ba, c_p2, sm.x, MZH_LD64, true, nullptr, lane, &c_h);
+      mzh_mma_store<MT, 4, 4, true, 16, 1>(fa, ba, c_p2, sm.x, MZH_LD64, true, nullptr, nullptr, lane, &c_h);
     } else {
-      mzh_mma_store<MT, 4, 4, true>(fa, ba, c_p2, sm.x, MZH_LD64, true, nullptr, lane);
+      mzh_mma_store<MT, 4, 4, true>(fa, ba, c_p2, sm.x, MZH_LD64, true, nullptr, nullptr, lane);
     }
     if (NEXT) {
       const MzhChunk c_n2 = mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64);
-      mzh_mma_store<MT, N2, 4, true, 16, 1>(fb, bb, c_p3, sm.x, MZH_LD64, true, nullptr, lane, &c_n2);
+      mzh_mma_store<MT, N2, 4, true, 16, 1>(fb, bb, c_p3, sm.x, MZH_LD64, true, nullptr, nullptr, lane, &c_n2);
     } else {
-      mzh_mma_store<MT, N2, 4, true>(fb, bb, c_p3, sm.x, MZH_LD64, true, nullptr, lane);
+      mzh_mma_store<MT, N2, 4, true>(fb, bb, c_p3, sm.x, MZH_LD64, true, nullptr, nullptr, lane);
     }
   }
   MZH_STAMP(9);
@@ -789,9 +818,10 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
       const MzhChunk c_h = mzh_head_chunk<R>(sm, net, wave);
       float* hin = wave == 0 ? sm.hidP : sm.hidV;
       if (NEXT)
-        mzh_mma_store<MT, 1, 16, true, 16, 4>(fa, ba, c_h, hin, MZH_LD256, false, nullptr, lane, &c_n1);  // pol2 / val2
+        mzh_mma_store<MT, 1, 16, true, 16, 4, true>(fa, ba, c_h, hin, MZH_LD256, false, nullptr, nullptr, lane,
+                                                    &c_n1);  // pol2 / val2
       else
-        mzh_mma_store<MT, 1, 16, true>(fa, ba, c_h, hin, MZH_LD256, false, nullptr, lane);
+        mzh_mma_store<MT, 1, 16, true, 0, 0, true>(fa, ba, c_h, hin, MZH_LD256, false, nullptr, nullptr, lane);
     } else if (NEXT) {
       mzh_fetch<4, 4, true>(fa, ba, c_n1, lane);  // next step's dyn0 chunk
     }

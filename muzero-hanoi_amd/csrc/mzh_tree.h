@@ -161,8 +161,8 @@ struct MzhTree {
       ucb = mzh_ucb(Nc, Wc, Rc, rb.P64[c], noised || p.np1, table[st.rootN[r]], disc, has, mmin, den, dinv, inv);
     }
     int pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
-    // the picking lane records the path entry and its own statistics; one shuffle of the
-    // packed (N | X << 16) word moves the selection on
+    // the picking lane records the path entry and its own statistics; the packed (N | X << 16)
+    // word of the pick, taken over the group's DPP tree, moves the selection on
     if (c == pick) {
       path[r * PL] = (uint16_t)pick;
       st.pc[r][0] = MzhPathEnt{Wc, Rc, Nc};
@@ -172,12 +172,13 @@ struct MzhTree {
     // (unconditional loads -- a lane without a child re-reads a valid block -- so the
     // compiler can count outstanding loads and wait only for the ones a level needs)
     int pf0 = *reinterpret_cast<const int*>(tb + (Xc >= 0 ? Xc : 0));
-    int nx = __shfl((Nc & 0xFFFF) | (Xc << 16), (lane & ~7) + pick);
+    int nx = mzh_group_take((Nc & 0xFFFF) | (Xc << 16), c == pick);
     int depth = 1, e = 0;
 
     // deeper levels: tree blocks in HBM (L2); lanes 6, 7 re-read slot 5 and act as
     // unexpanded, unvisited pads (N = 0, X = -1)
     const int cs = c < MZH_A ? c : MZH_A - 1;
+    MZH_LSTAMP_DECL
     while ((nx >> 16) >= 0) {
       e = nx >> 16;
       const int Np = nx & 0xFFFF;
@@ -187,6 +188,10 @@ struct MzhTree {
       Wc = b->W[cs];
       const float Pc = b->P[cs];
       if (c >= MZH_A) nxc = (int)0xFFFF0000;
+#ifdef MZH_STAMPS
+      asm volatile("" ::"v"(nxc), "v"(Rc), "v"(Pc), "v"(Wc));
+#endif
+      MZH_LSTAMP(0);
       // retire the previous level's prefetch (older than this level's block loads, so no
       // extra wait) -- keeps it in flight inside the loop
       asm volatile("" ::"v"(pf0));
@@ -195,14 +200,28 @@ struct MzhTree {
       Nc = nxc & 0xFFFF;
       ucb = c < MZH_A ? mzh_ucb(Nc, Wc, Rc, (double)Pc, p.np1, table[Np], disc, has, mmin, den, dinv, inv)
                       : -__builtin_inff();
+#ifdef MZH_STAMPS
+      asm volatile("" ::"v"(ucb));
+#endif
+      MZH_LSTAMP(1);
       pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
+#ifdef MZH_STAMPS
+      asm volatile("" ::"v"(pick));
+#endif
+      MZH_LSTAMP(2);
       if (c == pick) {
         path[r * PL + depth] = (uint16_t)(e * 8 + pick);
         if (depth < DC) st.pc[r][depth] = MzhPathEnt{Wc, Rc, Nc};
       }
-      nx = __shfl(nxc, (lane & ~7) + pick);
+      nx = mzh_group_take(nxc, c == pick);
       depth++;
+#ifdef MZH_STAMPS
+      asm volatile("" ::"v"(nx));
+#endif
+      MZH_LSTAMP(3);
+      MZH_LSTAMP_COUNT();
     }
+    MZH_LSTAMP_FLUSH(24);
     asm volatile("" ::"v"(pf0));
     if (c == 0) {
       st.depth[r] = depth;
