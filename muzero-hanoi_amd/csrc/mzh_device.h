@@ -566,9 +566,14 @@ __device__ __forceinline__ void mzh_normalize_par(const float* src, float* dst, 
 // interleaved on the same lanes (independent chains), the policy softmax alongside.  Lane q owns
 // logits k = q + 8i; max / exp / divide are lane-parallel, and both 33-term sums use the fixed
 // order of sum8_tree in the oracle: sequential per-lane partials combined by the DPP tree.
-template <int R, class SM>
-__device__ __forceinline__ void mzh_heads_row(SM& sm, int row, int q, int support, bool recurrent) {
-  const float lg = q < MZH_A ? sm.lpol[row * MZH_LDPOL + q] : -__builtin_inff();
+// SUP: the support size when the caller knows it at compile time (0: runtime `support`).  Logit
+// loads are unconditional (every k < 40 lies inside the row stride) and masked by selects, so
+// the head runs branch-free.
+template <int R, int SUP = 0, class SM>
+__device__ __forceinline__ void mzh_heads_row(SM& sm, int row, int q, int support_in, bool recurrent) {
+  const int support = SUP ? SUP : support_in;
+  const float lraw = sm.lpol[row * MZH_LDPOL + q];
+  const float lg = q < MZH_A ? lraw : -__builtin_inff();
   if (support == 1) {
     if (q == 0) {
       sm.value[row] = sm.lval[row * MZH_LDSUP];
@@ -584,7 +589,8 @@ __device__ __forceinline__ void mzh_heads_row(SM& sm, int row, int q, int suppor
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
       const int k = q + 8 * i;
-      e[h][i] = (h < nh && k < 33) ? lv[h][k] : -__builtin_inff();
+      const float raw = lv[h][k];
+      e[h][i] = (h < nh && k < 33) ? raw : -__builtin_inff();
       m[h] = e[h][i] > m[h] ? e[h][i] : m[h];
     }
   }

@@ -138,7 +138,7 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
       const int r = tr, c = tc;
       // this row's heads (networks.py:83,109,152-189) or its recorded network outputs
       if (!REPLAY) {
-        mzh_heads_row<R>(sm, r, c, net.support, true);
+        mzh_heads_row<R, SUP33 ? 33 : 0>(sm, r, c, net.support, true);
       } else {
         sm.pi[r * 8 + c] = (r < nvalid && c < MZH_A) ? p.rp_pi[((size_t)(root0 + r) * S + s) * MZH_A + c] : 0.0f;
         if (c == 0) {
