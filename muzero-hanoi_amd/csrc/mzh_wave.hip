@@ -331,16 +331,25 @@ __device__ __forceinline__ float mzw_ucb(int Nc, double Wc, float Rc, double P64
   const float u32 = p64_semantics ? (float)(P64 * w) : (float)P64 * (float)w;
   return q32 + u32;
 }
-// in-lane argmax over 6 children with the reference's tie handling (see mzh_group_pick)
-__device__ __forceinline__ int mzw_pick(const float (&u)[6], int tie, int& firstTie, int& extra) {
+// argmax over the 6 children with the reference's tie handling (see mzh_group_pick):
+// the 6 children are split over a lane pair (i, i + 32), 3 each: the pair's
+// max and its 6-bit argmax mask combine through v_permlane32_swap (max and OR are order-free), so
+// both lanes return the same pick and tie bookkeeping
+__device__ __forceinline__ int mzw_pick_pair(const float (&u)[3], int half, int tie, int& firstTie, int& extra) {
   float m = u[0];
-#pragma unroll
-  for (int c = 1; c < 6; ++c) m = u[c] > m ? u[c] : m;
+  m = u[1] > m ? u[1] : m;
+  m = u[2] > m ? u[2] : m;
+  float a, b;
+  mzw_pair32(m, a, b);
+  const float M = a > b ? a : b;
   int mask = 0;
 #pragma unroll
-  for (int c = 0; c < 6; ++c) mask |= (u[c] == m ? 1 : 0) << c;
-  const int cnt = __popc(mask);
-  const int first = __ffs(mask) - 1;
+  for (int j = 0; j < 3; ++j) mask |= (u[j] == M ? 1 : 0) << j;
+  mask <<= 3 * half;
+  const auto r = __builtin_amdgcn_permlane32_swap((unsigned)mask, (unsigned)mask, false, false);
+  const int full = (int)(r[0] | r[1]);
+  const int cnt = __popc(full);
+  const int first = __ffs(full) - 1;
   const bool six = (cnt == MZH_A) & (firstTie == 0);
   extra += ((cnt > 1) & !six) ? 1 : 0;
   firstTie |= six ? 1 : 0;
@@ -376,10 +385,13 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
   const bool noised = p.noise != nullptr;
   const size_t E = (size_t)p.E;
 
-  // root lanes: lane rho < ROOTS owns root wr0 + rho (tree phases)
-  const int rho = lane;
+  // root lanes: lanes rho and rho + 32 (rho < ROOTS) both own root wr0 + rho in the tree phases:
+  // selection splits the 6 children between them (3 UCBs per lane), every other tree step runs
+  // mirrored on both (same values, same addresses)
+  const int rho = lane & 31;
+  const int half = lane >> 5;
   const int rroot = wr0 + rho;
-  const bool rvalid = lane < ROOTS && rroot < p.B;
+  const bool rvalid = rho < ROOTS && rroot < p.B;
   MzwBlock* tb = reinterpret_cast<MzwBlock*>(p.tree) + (size_t)(rvalid ? rroot : 0) * E;
   double mmax = -__builtin_inf(), mmin = __builtin_inf();
   if (rvalid && p.minmax_in) {
@@ -480,13 +492,15 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
     // ---------------- select (mcts.py:75-86; node.py:72-123): one lane per root ----------------
     if (rvalid) {
       const bool has = mmax > mmin;
-      float u[6];
+      float u[3];
       const double tr = table[rootN];
 #pragma unroll
-      for (int c = 0; c < MZH_A; ++c)
-        u[c] = mzw_ucb(ws.rN[c][rho], ws.rW[c][rho], ws.rR[c][rho], ws.rP[c][rho], noised || p.np1, tr, disc, has,
+      for (int j = 0; j < 3; ++j) {
+        const int c = 3 * half + j;
+        u[j] = mzw_ucb(ws.rN[c][rho], ws.rW[c][rho], ws.rR[c][rho], ws.rP[c][rho], noised || p.np1, tr, disc, has,
                        mmin, den, dinv, inv);
-      int pick = mzw_pick(u, tie, firstTie, extra);
+      }
+      int pick = mzw_pick_pair(u, half, tie, firstTie, extra);
       int Np = ws.rN[pick][rho], X = ws.rX[pick][rho];
       ws.path[0][rho] = (uint16_t)pick;
       ws.pcW[0][rho] = ws.rW[pick][rho];
@@ -511,10 +525,18 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
         for (int c = 0; c < MZH_A; ++c) {
           Rc[c] = __int_as_float(dw[6 + c]);
           Wc[c] = __hiloint2double(dw[19 + 2 * c], dw[18 + 2 * c]);
-          u[c] = mzw_ucb(dw[c] & 0xFFFF, Wc[c], Rc[c], (double)__int_as_float(dw[12 + c]), p.np1, table[Np], disc, has,
-                         mmin, den, dinv, inv);
         }
-        pick = mzw_pick(u, tie, firstTie, extra);
+        const double tn = table[Np];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          // this lane's three children (dw is the whole block on both lanes)
+          const int nxj = half ? dw[3 + j] : dw[j];
+          const float Rj = half ? Rc[3 + j] : Rc[j];
+          const double Wj = half ? Wc[3 + j] : Wc[j];
+          const float Pj = __int_as_float(half ? dw[15 + j] : dw[12 + j]);
+          u[j] = mzw_ucb(nxj & 0xFFFF, Wj, Rj, (double)Pj, p.np1, tn, disc, has, mmin, den, dinv, inv);
+        }
+        pick = mzw_pick_pair(u, half, tie, firstTie, extra);
         int nx = dw[0];
         double Wp = Wc[0];
         float Rp = Rc[0];
@@ -642,7 +664,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
         rr = rew[0];
 #pragma unroll
         for (int n = 1; n < NT; ++n)
-          if ((lane >> 4) == n) {
+          if ((rho >> 4) == n) {
             vv = val[n];
             rr = rew[n];
           }
@@ -732,7 +754,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
   }
 
   // ---------------- results (mcts.py:111-126, 154-176) ----------------
-  if (!rvalid) return;
+  if (!rvalid || half) return;
   const int root = rroot;
   int vis[MZH_A];
   for (int a = 0; a < MZH_A; ++a) {
