@@ -30,10 +30,10 @@ def main():
     from bench import random_roots
     obs = torch.from_numpy(random_roots(4, B, 1)).cuda()
     noise, tie, u = (torch.from_numpy(x).cuda() for x in rng.synthetic_draws(B, deterministic=False, alpha=0.25, seed=1))
-    eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, kernel="wave")
+    eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, kernel=os.environ.get("MZH_PROBE_KERNEL", "wave"))
     torch.cuda.synchronize()
     L.mzh_diag_wave_stamps(buf.ctypes.data)
-    eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, kernel="wave")
+    eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, kernel=os.environ.get("MZH_PROBE_KERNEL", "wave"))
     torch.cuda.synchronize()
     L.mzh_diag_wave_stamps(buf.ctypes.data)
     per = buf[:8, :5] / S  # 8 waves (ping-pong workgroup); the 4-wave build leaves rows 4-7 zero
