@@ -117,7 +117,7 @@ extern "C" int mzh_create(int device, int n_disks, int max_sims, int max_roots, 
   eng->kin = ((eng->in_dim + 15) / 16) * 16;
   eng->E = max_sims + 1;
   const size_t nblk = (size_t)max_roots * eng->E;
-  // MzhBlock: one cache line per node (MZW_QC builds: two, see mzh_wave.hip MzwNodeQ)
+  // MzhBlock (mzh_tree.h) / MzwBlock (mzh_wave.hip): one 128-B cache line per expanded node
   hipError_t e = hipMalloc(&eng->tree, nblk * 128);  // one 128-B block per expanded node
   if (e == hipSuccess) e = hipMalloc(&eng->htree, nblk * MZH_LATENT * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&eng->pathx, nblk * sizeof(uint16_t));

@@ -16,13 +16,18 @@ struct MzhNX {
   uint16_t N;  // child visit count (node.py:21)
   int16_t X;   // expanded-node index of the child, -1 = not expanded (node.py:19 is_expanded)
 };
+// one child's selection operands except W, slot-major: N | X, reward and prior in one dwordx3
+struct MzhSlot {
+  MzhNX nx;
+  float R;  // child reward (python float of an fp32 value, node.py:25)
+  float P;  // child prior, fp32 (node.py:16)
+};
 struct __align__(128) MzhBlock {
-  MzhNX nx[6];  // N and X adjacent: one dword load per child in selection
-  float R[6];   // child reward (python float of an fp32 value, node.py:25)
-  float P[6];   // child prior, fp32 (node.py:16)
-  double W[6];  // child summed value, fp64 (node.py:22)
+  MzhSlot sl[6];  // 72 B
+  double W[6];    // child summed value, fp64 (node.py:22)
   uint32_t pad[2];
 };
+static_assert(sizeof(MzhSlot) == 12, "slot layout");
 static_assert(sizeof(MzhBlock) == 128, "block layout");
 static_assert(__builtin_offsetof(MzhBlock, W) == 72, "block layout");
 
@@ -183,10 +188,11 @@ struct MzhTree {
       e = nx >> 16;
       const int Np = nx & 0xFFFF;
       const MzhBlock* b = tb + e;
-      int nxc = *reinterpret_cast<const int*>(&b->nx[cs]);
-      Rc = b->R[cs];
+      const uint3 sv = *reinterpret_cast<const uint3*>(&b->sl[cs]);  // N | X, R, P: one dwordx3
+      int nxc = (int)sv.x;
+      Rc = __uint_as_float(sv.y);
       Wc = b->W[cs];
-      const float Pc = b->P[cs];
+      const float Pc = __uint_as_float(sv.z);
       if (c >= MZH_A) nxc = (int)0xFFFF0000;
 #ifdef MZH_STAMPS
       asm volatile("" ::"v"(nxc), "v"(Rc), "v"(Pc), "v"(Wc));
@@ -264,9 +270,9 @@ struct MzhTree {
     }
     MzhBlock* nb = tb + enew;  // the new expanded node's 6 children (node.py:44-49)
     if (c < MZH_A) {
-      *reinterpret_cast<uint32_t*>(&nb->nx[c]) = 0xFFFF0000u;  // N = 0, X = -1
-      nb->R[c] = 0.0f;
-      nb->P[c] = sm.pi[r * 8 + c];
+      *reinterpret_cast<uint32_t*>(&nb->sl[c].nx) = 0xFFFF0000u;  // N = 0, X = -1
+      nb->sl[c].R = 0.0f;
+      nb->sl[c].P = sm.pi[r * 8 + c];
       nb->W[c] = 0.0;
     }
     const int le = st.leafE[r], la = st.leafA[r], depth = st.depth[r];
@@ -277,19 +283,19 @@ struct MzhTree {
         rb.X[la] = enew;
         rb.R[la] = rew;
       } else {
-        tb[le].nx[la].X = (int16_t)enew;
-        tb[le].R[la] = rew;
+        tb[le].sl[la].nx.X = (int16_t)enew;
+        tb[le].sl[la].R = rew;
       }
       double v = (double)sm.value[r];
       int j = depth - 1;
       for (; j >= DC; --j) {  // beyond the LDS path cache (rare): update here from HBM
         const int slot = path[r * PL + j];
         const int e = slot >> 3, a = slot & 7;
-        const double rw = (j == depth - 1) ? (double)rew : (double)tb[e].R[a];
+        const double rw = (j == depth - 1) ? (double)rew : (double)tb[e].sl[a].R;
         const double W = tb[e].W[a] + v;
-        const int N = tb[e].nx[a].N + 1;
+        const int N = tb[e].sl[a].nx.N + 1;
         tb[e].W[a] = W;
-        tb[e].nx[a].N = (uint16_t)N;
+        tb[e].sl[a].nx.N = (uint16_t)N;
         const double q = rw + disc * mzh_div(W, (double)N, inv[N]);
         lmax = q > lmax ? q : lmax;
         lmin = q < lmin ? q : lmin;
@@ -329,7 +335,7 @@ struct MzhTree {
         rb.N[a] = N;
       } else {
         tb[e].W[a] = W;
-        tb[e].nx[a].N = (uint16_t)N;
+        tb[e].sl[a].nx.N = (uint16_t)N;
       }
       const double q = rw + disc * mzh_div(W, (double)N, inv[N]);
       lmax = q > lmax ? q : lmax;
