@@ -68,6 +68,7 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
     st.extra[r] = 0;
     st.steps[r] = 0;
     st.depth[r] = 0;
+    st.tie[r] = (p.tie_idx && r < nvalid) ? p.tie_idx[root0 + r] : 0;
     if (p.minmax_in && r < nvalid) {
       mzh_mm_set(st.mm[r], p.minmax_in[2 * (root0 + r)], p.minmax_in[2 * (root0 + r) + 1]);
     } else {
@@ -154,6 +155,7 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
         if (s + 1 < S) {
           group_sync();
           tree.select(r, c, s + 1);
+          MZH_STAMP(30);
         }
       }
     }

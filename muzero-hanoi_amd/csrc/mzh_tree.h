@@ -64,7 +64,7 @@ struct SearchSmem {
   int leafE[R];
   int leafA[R];
   int steps[R];
-  int pad_[R];
+  int tie[R];  // the host-drawn index for the first 6-way tie (tie_idx)
 };
 
 // a / b correctly rounded from y = RN(1/b) (Markstein: q = RN(a*y) is within one ulp, the fma
@@ -151,7 +151,12 @@ struct MzhTree {
     const bool has = mmax > mmin;
     int firstTie = st.firstTie[r];
     int extra = st.extra[r];
-    const int tie = p.tie_idx ? p.tie_idx[root0 + r] : 0;
+    const int tie = st.tie[r];
+    MZH_STAMP_DECL
+#ifdef MZH_STAMPS
+    asm volatile("" ::"v"(tie), "v"(dinv));
+#endif
+    MZH_STAMP(13);
     // level 0: the root block (LDS)
     int Nc = 0, Xc = -1;
     double Wc = 0.0;
@@ -183,6 +188,10 @@ struct MzhTree {
     // deeper levels: tree blocks in HBM (L2); lanes 6, 7 re-read slot 5 and act as
     // unexpanded, unvisited pads (N = 0, X = -1)
     const int cs = c < MZH_A ? c : MZH_A - 1;
+#ifdef MZH_STAMPS
+    asm volatile("" ::"v"(nx), "v"(pf0));
+#endif
+    MZH_STAMP(14);
     MZH_LSTAMP_DECL
     while ((nx >> 16) >= 0) {
       e = nx >> 16;
@@ -228,6 +237,7 @@ struct MzhTree {
       MZH_LSTAMP_COUNT();
     }
     MZH_LSTAMP_FLUSH(24);
+    MZH_STAMP(15);
     asm volatile("" ::"v"(pf0));
     if (c == 0) {
       st.depth[r] = depth;
@@ -248,6 +258,7 @@ struct MzhTree {
         d[4] = h1[0]; d[5] = h1[1]; d[6] = h1[2]; d[7] = h1[3];
       }
       if (c == 0) sm.act[r] = pick;
+      MZH_STAMP(31);
     }
   }
 
@@ -259,6 +270,7 @@ struct MzhTree {
     MzhBlock* tb = reinterpret_cast<MzhBlock*>(p.tree) + (size_t)(root0 + r) * p.E;
     MzhRootBlk& rb = st.root[r];
     const int enew = s + 1;
+    MZH_STAMP_DECL
     if (!REPLAY) {
       // the new node's latent (read back when one of its children is expanded -- usually
       // within a few simulations on the deepening path, so it stays cacheable)
@@ -275,6 +287,7 @@ struct MzhTree {
       nb->sl[c].P = sm.pi[r * 8 + c];
       nb->W[c] = 0.0;
     }
+    MZH_STAMP(16);
     const int le = st.leafE[r], la = st.leafA[r], depth = st.depth[r];
     const float rew = sm.reward[r];
     double lmax = -__builtin_inf(), lmin = __builtin_inf();
@@ -319,6 +332,7 @@ struct MzhTree {
       lmax = q > lmax ? q : lmax;
       lmin = q < lmin ? q : lmin;
     }
+    MZH_STAMP(17);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -341,11 +355,13 @@ struct MzhTree {
       lmax = q > lmax ? q : lmax;
       lmin = q < lmin ? q : lmin;
     }
+    MZH_STAMP(18);
     mzh_maxmin8d(lmax, lmin);
     if (c == 0) {
       const double mx = st.mm[r][0], mn = st.mm[r][1];
       mzh_mm_set(st.mm[r], lmax > mx ? lmax : mx, lmin < mn ? lmin : mn);
     }
+    MZH_STAMP(29);
   }
 
   // ---------------- results of root r (mcts.py:111-126, 154-176), one lane ----------------

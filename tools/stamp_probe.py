@@ -17,8 +17,10 @@ from muzero_hanoi_amd.networks import MuZeroNet  # noqa: E402
 
 MLP = {0: "prologue", 1: "dyn0", 2: "bar+fetch", 3: "dyn2", 4: "bar+fetch", 5: "norm", 6: "rwd0", 7: "bar+fetch",
        8: "rwd2|pred4", 9: "pred4+pred3", 10: "bar+pol2/val2", 11: "bar+heads", 12: "bar"}
-SEARCH = {16: "select:start", 29: "select:root level", 30: "select:loop", 17: "select:gather", 18: "(unused)",
-          19: "bar->mlp", 20: "mlp", 21: "heads", 22: "expand+backup", 23: "bar"}
+SEARCH = {16: "backup:latent+new-block stores", 17: "backup:value chain (lane 0)", 18: "backup:path updates",
+          29: "backup:min-max reduce+set", 13: "select:setup (mm, tie load)", 14: "select:root level+prefetch",
+          15: "select:level loop", 31: "select:bookkeeping+latent gather", 30: "select (own group)", 19: "bar->mlp", 20: "mlp", 21: "heads",
+          22: "expand+backup", 23: "bar (select of the slowest group)"}
 
 
 def main():
@@ -55,7 +57,7 @@ def main():
     L.mzh_diag_stamps(buf.ctypes.data)
     per = buf / S
     out["search_per_sim"] = {f"{k}:{v}": per[:4, k].tolist() for k, v in SEARCH.items()}
-    out["search_per_sim_total"] = (per[:4, 16:24].sum(1) + per[:4, 29] + per[:4, 30]).tolist()
+    out["search_per_sim_total"] = (per[:4, 19:24].sum(1) + per[:4, 30]).tolist()  # 16-18, 29 split 22
     lv = {24: "mem(block)", 25: "ucb", 26: "pick", 27: "path+shfl"}
     its = per[:4, 28] * S
     out["select_level_ticks"] = {f"{k}:{v}": (per[:4, k] * S / np.maximum(its, 1)).round().tolist() for k, v in lv.items()}
