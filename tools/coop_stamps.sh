@@ -1,3 +1,4 @@
+# phase stamps of the cooperative search kernel at 8,192 / 4,096 roots (needs libmzh_diag.so: python -m muzero_hanoi_amd.build --diag)
 set -e
 mkdir -p gpurun_out
 for B in 8192 4096; do timeout -k 10 120 python tools/stamp_probe.py $B > gpurun_out/stamps_$B.json; done
