@@ -39,6 +39,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (matrix), spec
+# measured ceiling of back-to-back v_mfma_f32_16x16x4_f32 with distinct register operands, by waves per
+# SIMD (tools/micro/lds_a_probe.hip, profiles/r02s2_mfma_ceiling.json): informational, beside the spec
+# peak that `frac` is priced against
+FP32_MFMA_MEASURED_TFLOPS = {1: 144.0, 2: 150.7}
 HBM_PEAK_GBPS = 8000.0         # MI355X_MICROARCH.md: HBM3E peak (spec)
 MLP_FLOP_PER_SIM = 203_776     # recurrent_inference matmul FLOPs (2 x 101,888 MAC)
 # SURVEY.md 8d tree bytes: 124 B per selection step, 28 B per backed-up path node, 540 B per expansion
@@ -353,6 +357,10 @@ def main():
     flops_launch = B * (S * MLP_FLOP_PER_SIM + root_flops(N))
     achieved = flops_launch / (kern_ms * 1e-3) / 1e12
     kname = kernel_name(a.kernel, B)[1].format(r="false")
+    # waves sharing a SIMD: the wave kernel runs B / (16 NT) waves, two workgroups of 4 per CU at most;
+    # the cooperative kernel one 4-wave workgroup per CU
+    nt = 2 if kname.startswith("mzh_wave_kernel<2") else 1 if kname.startswith("mzh_wave_kernel<1") else 0
+    wps = 1 if nt == 0 else min(2, max(1, -(-B // (16 * nt * 1024))))
     traffic = None
     if os.path.exists(a.traffic_json):
         try:
@@ -389,7 +397,14 @@ def main():
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": kname, "kernel_ms": kern_ms,
-                     "flop_per_launch": flops_launch, "sel_steps_per_sim": sel_sum / (B * S), "tree": tree},
+                     "flop_per_launch": flops_launch, "sel_steps_per_sim": sel_sum / (B * S),
+                     "measured_ceiling": {"value": FP32_MFMA_MEASURED_TFLOPS[wps],
+                                          "frac": achieved / FP32_MFMA_MEASURED_TFLOPS[wps],
+                                          "waves_per_simd": wps,
+                                          "what": "back-to-back MFMAs with distinct register operands at this "
+                                                  "kernel's waves per SIMD (tools/micro/lds_a_probe.hip); "
+                                                  "informational -- frac above is against the spec peak"},
+                     "tree": tree},
         "cpu_baseline": cpu,
     }
     if rank == 0:
