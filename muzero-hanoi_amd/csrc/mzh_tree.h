@@ -83,12 +83,15 @@ __device__ __forceinline__ double mzh_normalize(double v, bool has, double mn, d
 }
 
 // ucb = fl32(Q) + fl32(U) for one child (node.py:90-123); `tnp` = table[N_parent], inv[k] = RN(1/k)
+// Branch-free: both reciprocals are read together (one ds_read2_b64) and the Q and U chains run side
+// by side; for Nc = 0 the Q chain computes from inv[0] = inf and its result is discarded.
 __device__ __forceinline__ float mzh_ucb(int Nc, double Wc, float Rc, double P64, bool p64_semantics, double tnp,
                                          double disc, bool has, double mn, double den, double dinv,
                                          const double* inv) {
-  float q32 = 0.0f;
-  if (Nc > 0) q32 = (float)mzh_normalize((double)Rc + disc * mzh_div(Wc, (double)Nc, inv[Nc]), has, mn, den, dinv);
-  const double w = mzh_div(tnp, (double)(Nc + 1), inv[Nc + 1]);
+  const double i0 = inv[Nc], i1 = inv[Nc + 1];
+  const double qn = mzh_normalize((double)Rc + disc * mzh_div(Wc, (double)Nc, i0), has, mn, den, dinv);
+  const float q32 = Nc > 0 ? (float)qn : 0.0f;
+  const double w = mzh_div(tnp, (double)(Nc + 1), i1);
   // np.float64 priors (Dirichlet-mixed root) or NumPy-1 promotion: fl32(fl64(prior * w));
   // NumPy-2 with np.float32 priors: fl32(prior * fl32(w))
   const float u32 = p64_semantics ? (float)(P64 * w) : (float)P64 * (float)w;
@@ -161,14 +164,15 @@ struct MzhTree {
     int Nc = 0, Xc = -1;
     double Wc = 0.0;
     float Rc = 0.0f;
-    float ucb = -__builtin_inff();
-    if (c < MZH_A) {
+    float ucb;
+    {  // all 8 slots of the root block are initialised (slots 6, 7: N = 0, X = -1, prior 0)
       const MzhRootBlk& rb = st.root[r];
       Nc = rb.N[c];
       Xc = rb.X[c];
       Wc = rb.W[c];
       Rc = rb.R[c];
-      ucb = mzh_ucb(Nc, Wc, Rc, rb.P64[c], noised || p.np1, table[st.rootN[r]], disc, has, mmin, den, dinv, inv);
+      const float u = mzh_ucb(Nc, Wc, Rc, rb.P64[c], noised || p.np1, table[st.rootN[r]], disc, has, mmin, den, dinv, inv);
+      ucb = c < MZH_A ? u : -__builtin_inff();
     }
     int pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
     // the picking lane records the path entry and its own statistics; the packed (N | X << 16)
@@ -198,6 +202,7 @@ struct MzhTree {
       const int Np = nx & 0xFFFF;
       const MzhBlock* b = tb + e;
       const uint3 sv = *reinterpret_cast<const uint3*>(&b->sl[cs]);  // N | X, R, P: one dwordx3
+      const double tnp = table[Np];  // LDS: in flight beside the block loads
       int nxc = (int)sv.x;
       Rc = __uint_as_float(sv.y);
       Wc = b->W[cs];
@@ -213,8 +218,10 @@ struct MzhTree {
       const int xc = nxc >> 16;
       pf0 = *reinterpret_cast<const int*>(tb + (xc >= 0 ? xc : e));
       Nc = nxc & 0xFFFF;
-      ucb = c < MZH_A ? mzh_ucb(Nc, Wc, Rc, (double)Pc, p.np1, table[Np], disc, has, mmin, den, dinv, inv)
-                      : -__builtin_inff();
+      {
+        const float u = mzh_ucb(Nc, Wc, Rc, (double)Pc, p.np1, tnp, disc, has, mmin, den, dinv, inv);
+        ucb = c < MZH_A ? u : -__builtin_inff();
+      }
 #ifdef MZH_STAMPS
       asm volatile("" ::"v"(ucb));
 #endif
@@ -314,15 +321,21 @@ struct MzhTree {
         lmin = q < lmin ? q : lmin;
         v = rw + disc * v;
       }
-      if (j == depth - 1 && j >= 0) {  // the leaf (its reward was just set)
-        st.bval[r][j] = v;
-        v = (double)rew + disc * v;
-        --j;
-      }
-#pragma unroll 4
-      for (; j >= 0; --j) {
-        st.bval[r][j] = v;
-        v = (double)st.pc[r][j].R + disc * v;
+      // the LDS-cached depths j <= jtop: every reward snapshot is read up front, then the fp64
+      // chain runs in registers (the leaf takes its new reward); a step above this lane's jtop
+      // keeps v, and steps above every active lane's jtop are skipped (wave-uniform branch).
+      // bval entries at depths >= `depth` are written but never read.
+      const int jtop = j;
+      float Rj[DC];
+#pragma unroll
+      for (int jj = 0; jj < DC; ++jj) Rj[jj] = st.pc[r][jj].R;
+#pragma unroll
+      for (int jj = DC - 1; jj >= 0; --jj) {
+        if (!__any(jj <= jtop)) continue;
+        st.bval[r][jj] = v;
+        const double rw = jj == depth - 1 ? (double)rew : (double)Rj[jj];
+        const double vn = rw + disc * v;
+        v = jj <= jtop ? vn : v;
       }
       const double W = st.rootW[r] + v;
       const int N = st.rootN[r] + 1;
