@@ -97,7 +97,13 @@ __device__ __forceinline__ float mzh_signed_parabolic(float x) {
   t = 1.0f + t;
   t = __builtin_sqrtf(t);
   t = t / 2.0f;
-  t = t / 0.001000000047497451305389404296875f;
+  {  // t / 0.001f (t >= 0.5 here) by Markstein from y = RN(1/0.001f): equal to the IEEE quotient
+     // for every float t >= 0.5 whose quotient is finite (checked exhaustively, tools/markstein_c.c)
+    const float b = 0.001000000047497451305389404296875f, y = 0x1.f3fffep+9f;
+    const float q = t * y;
+    const float r = __builtin_fmaf(-q, b, t);
+    t = __builtin_fmaf(r, y, q);
+  }
   float z = t - 500.0f;
   float sg = x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f);
   return sg * (z * z - 1.0f);
@@ -105,15 +111,17 @@ __device__ __forceinline__ float mzh_signed_parabolic(float x) {
 
 // ------------------------------------------------------------------------------------------
 // 8-lane DPP reductions (aligned groups of 8 lanes; no LDS crossbar).  Steps: quad_perm
-// [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror (lane i <-> 7-i).  Every lane of the group ends
+// [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror (lane i <-> 7-i).  Every source lane lies in the
+// reading lane's own 8-lane group, whose lanes are always active together, so bound_ctrl = 1 changes
+// nothing but lets the compiler fold each move into its consumer (v_add_f32_dpp, v_or_b32_dpp).  Every lane of the group ends
 // with the same bits: IEEE add/max are commutative, so the sum is exactly
 // ((s0+s1)+(s2+s3)) + ((s4+s5)+(s6+s7)) on every lane -- the order oracle/mzh_oracle.c uses.
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ float mzh_dpp_f(float v, int ctrl_sel) {
   switch (ctrl_sel) {
-    case 0: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
-    case 1: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
-    default: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));
+    case 0: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
+    case 1: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true));
+    default: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, true));
   }
 }
 __device__ __forceinline__ float mzh_max8(float v) {
@@ -123,6 +131,16 @@ __device__ __forceinline__ float mzh_max8(float v) {
     v = t > v ? t : v;
   }
   return v;
+}
+// max over the group for NaN-free values (UCB scores: finite or -inf): one v_max_f32_dpp per step
+// instead of move + compare + select (fmaxf would add canonicalising maxes in IEEE mode).  A max of
+// +0 and -0 may return either zero; the callers only compare for equality, where they are equal.
+__device__ __forceinline__ float mzh_max8_nonan(float v) {
+  float a, b, c;
+  asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(a) : "v"(v));
+  asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %1, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf" : "=v"(b) : "v"(a));
+  asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %1, %1 row_half_mirror row_mask:0xf bank_mask:0xf" : "=v"(c) : "v"(b));
+  return c;
 }
 __device__ __forceinline__ float mzh_min8(float v) {
 #pragma unroll
@@ -142,9 +160,9 @@ __device__ __forceinline__ float mzh_sum8(float v) {
 // (an OR over the DPP tree: three VALU steps instead of a ds_bpermute round trip)
 __device__ __forceinline__ int mzh_group_take(int v, bool sel) {
   int x = sel ? v : 0;
-  x |= __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);
-  x |= __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);
-  x |= __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false);
+  x |= __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true);
+  x |= __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, true);
+  x |= __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, true);
   return x;
 }
 
@@ -154,16 +172,16 @@ __device__ __forceinline__ double mzh_dpp_d(double v, int ctrl_sel) {
   int l2, h2;
   switch (ctrl_sel) {
     case 0:
-      l2 = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, false);
-      h2 = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false);
+      l2 = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, true);
+      h2 = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, true);
       break;
     case 1:
-      l2 = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xF, 0xF, false);
-      h2 = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xF, 0xF, false);
+      l2 = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xF, 0xF, true);
+      h2 = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xF, 0xF, true);
       break;
     default:
-      l2 = __builtin_amdgcn_mov_dpp(lo, 0x141, 0xF, 0xF, false);
-      h2 = __builtin_amdgcn_mov_dpp(hi, 0x141, 0xF, 0xF, false);
+      l2 = __builtin_amdgcn_mov_dpp(lo, 0x141, 0xF, 0xF, true);
+      h2 = __builtin_amdgcn_mov_dpp(hi, 0x141, 0xF, 0xF, true);
       break;
   }
   return __longlong_as_double(((long long)h2 << 32) | (unsigned)l2);

@@ -111,7 +111,7 @@ __device__ __forceinline__ void mzh_mm_set(double* mm, double mx, double mn) {
 // is counted (RNG-stream divergence) and resolved to the lowest index.  Branch-free; every lane
 // of the group returns the same pick.
 __device__ __forceinline__ int mzh_group_pick(float ucb, int c, int lane, int tie, int& firstTie, int& extra) {
-  const float m = mzh_max8(ucb);
+  const float m = mzh_max8_nonan(ucb);
   const unsigned long long bal = __ballot(c < MZH_A && ucb == m);
   const unsigned mask = (unsigned)(bal >> (lane & ~7)) & 0x3Fu;
   const int cnt = __popc(mask);
@@ -245,7 +245,6 @@ struct MzhTree {
     }
     MZH_LSTAMP_FLUSH(24);
     MZH_STAMP(15);
-    asm volatile("" ::"v"(pf0));
     if (c == 0) {
       st.depth[r] = depth;
       st.leafE[r] = e;
@@ -267,6 +266,9 @@ struct MzhTree {
       if (c == 0) sm.act[r] = pick;
       MZH_STAMP(31);
     }
+    // the last level's prefetch is retired only here, so the latent loads above issue at the loop
+    // exit instead of behind a wait for it (loads complete in issue order either way)
+    asm volatile("" ::"v"(pf0));
   }
 
   // ---------------- expand bookkeeping + backup (node.py:30-70) of simulation s ----------------

@@ -322,12 +322,13 @@ __device__ __forceinline__ double mzw_div(double a, double b, double y) {
 __device__ __forceinline__ float mzw_ucb(int Nc, double Wc, float Rc, double P64, bool p64_semantics, double tnp,
                                          double disc, bool has, double mn, double den, double dinv,
                                          const double* inv) {
-  float q32 = 0.0f;
-  if (Nc > 0) {
-    const double v = (double)Rc + disc * mzw_div(Wc, (double)Nc, inv[Nc]);
-    q32 = (float)(has ? mzw_div(v - mn, den, dinv) : v);
-  }
-  const double w = mzw_div(tnp, (double)(Nc + 1), inv[Nc + 1]);
+  // branch-free: both reciprocals in one LDS read, the Q and U chains side by side (for Nc = 0 the
+  // Q chain runs on inv[0] = inf and is discarded)
+  const double i0 = inv[Nc], i1 = inv[Nc + 1];
+  const double v = (double)Rc + disc * mzw_div(Wc, (double)Nc, i0);
+  const double qn = has ? mzw_div(v - mn, den, dinv) : v;
+  const float q32 = Nc > 0 ? (float)qn : 0.0f;
+  const double w = mzw_div(tnp, (double)(Nc + 1), i1);
   const float u32 = p64_semantics ? (float)(P64 * w) : (float)P64 * (float)w;
   return q32 + u32;
 }
