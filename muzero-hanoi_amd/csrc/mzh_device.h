@@ -587,15 +587,23 @@ __device__ __forceinline__ void mzh_normalize_par(const float* src, float* dst, 
 // SUP: the support size when the caller knows it at compile time (0: runtime `support`).  Logit
 // loads are unconditional (every k < 40 lies inside the row stride) and masked by selects, so
 // the head runs branch-free.
-template <int R, int SUP = 0, class SM>
-__device__ __forceinline__ void mzh_heads_row(SM& sm, int row, int q, int support_in, bool recurrent) {
+// The row's results also come back in registers (MzhHeadOut: lane q's policy probability; value and
+// reward on lane 0); STORE = false skips the LDS copies (the search kernel keeps them in registers).
+struct MzhHeadOut {
+  float pp, value, reward;
+};
+template <int R, int SUP = 0, bool STORE = true, class SM>
+__device__ __forceinline__ MzhHeadOut mzh_heads_row(SM& sm, int row, int q, int support_in, bool recurrent) {
   const int support = SUP ? SUP : support_in;
   const float lraw = sm.lpol[row * MZH_LDPOL + q];
   const float lg = q < MZH_A ? lraw : -__builtin_inff();
+  MzhHeadOut out{0.0f, 0.0f, 0.0f};
   if (support == 1) {
-    if (q == 0) {
-      sm.value[row] = sm.lval[row * MZH_LDSUP];
-      sm.reward[row] = recurrent ? sm.lrwd[row * MZH_LDSUP] : 0.0f;
+    out.value = sm.lval[row * MZH_LDSUP];
+    out.reward = recurrent ? sm.lrwd[row * MZH_LDSUP] : 0.0f;
+    if (STORE && q == 0) {
+      sm.value[row] = out.value;
+      sm.reward[row] = out.reward;
     }
   }
   const int nh = support == 1 ? 0 : (recurrent ? 2 : 1);
@@ -650,7 +658,8 @@ __device__ __forceinline__ void mzh_heads_row(SM& sm, int row, int q, int suppor
 #pragma unroll
       for (int i = 0; i < 5; ++i) pk[h][i] = e[h][i] / sh[h];
   }
-  if (q < MZH_A) sm.pi[row * 8 + q] = pp;
+  out.pp = q < MZH_A ? pp : 0.0f;
+  if (STORE && q < MZH_A) sm.pi[row * 8 + q] = pp;
   float x[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -666,10 +675,15 @@ __device__ __forceinline__ void mzh_heads_row(SM& sm, int row, int q, int suppor
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) x[h] = mzh_sum8(x[h]);
-  if (q == 0 && nh > 0) {
-    sm.value[row] = mzh_signed_parabolic(x[0]);
-    sm.reward[row] = nh > 1 ? mzh_signed_parabolic(x[1]) : 0.0f;
+  if (nh > 0) {
+    out.value = mzh_signed_parabolic(x[0]);
+    out.reward = nh > 1 ? mzh_signed_parabolic(x[1]) : 0.0f;
+    if (STORE && q == 0) {
+      sm.value[row] = out.value;
+      sm.reward[row] = out.reward;
+    }
   }
+  return out;
 }
 
 // all rows: 8 lanes per row, row = tid / 8 (32 rows over 256 threads)

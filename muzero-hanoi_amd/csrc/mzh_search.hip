@@ -125,8 +125,13 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
     __builtin_amdgcn_wave_barrier();
   };
 
+  // the root's state lives in its group's registers from here to the results
+  MzhRootReg rs;
+  const bool town = tgroup && tr < nvalid;
+  if (town) rs.load(st, tr);
+
   MZH_STAMP_DECL
-  if (tgroup && tr < nvalid) tree.select(tr, tc, 0);
+  if (town) tree.select(tr, tc, 0, rs);
   __syncthreads();
   for (int s = 0; s < S; ++s) {
     // ---------------- expand via the network (mcts.py:88-106) ----------------
@@ -135,28 +140,25 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
       mzh_mlp_recurrent_body<R, true, N2, false>(sm, net, wave, lane, fa, ba, fb, bb, OHL ? ohl : net.dyn0_onehot);
       MZH_STAMP(20);
     }
-    if (tgroup) {
+    if (town) {
       const int r = tr, c = tc;
-      // this row's heads (networks.py:83,109,152-189) or its recorded network outputs
+      // this row's heads (networks.py:83,109,152-189) or its recorded network outputs, in registers
+      MzhHeadOut ho;
       if (!REPLAY) {
-        mzh_heads_row<R, SUP33 ? 33 : 0>(sm, r, c, net.support, true);
+        ho = mzh_heads_row<R, SUP33 ? 33 : 0, false>(sm, r, c, net.support, true);
       } else {
-        sm.pi[r * 8 + c] = (r < nvalid && c < MZH_A) ? p.rp_pi[((size_t)(root0 + r) * S + s) * MZH_A + c] : 0.0f;
-        if (c == 0) {
-          sm.value[r] = r < nvalid ? p.rp_value[(size_t)(root0 + r) * S + s] : 0.0f;
-          sm.reward[r] = r < nvalid ? p.rp_reward[(size_t)(root0 + r) * S + s] : 0.0f;
-        }
+        const size_t rs_i = (size_t)(root0 + r) * S + s;
+        ho.pp = c < MZH_A ? p.rp_pi[rs_i * MZH_A + c] : 0.0f;
+        ho.value = p.rp_value[rs_i];
+        ho.reward = p.rp_reward[rs_i];
       }
-      group_sync();
       MZH_STAMP(21);
-      if (r < nvalid) {
-        tree.backup(r, c, s);
-        MZH_STAMP(22);
-        if (s + 1 < S) {
-          group_sync();
-          tree.select(r, c, s + 1);
-          MZH_STAMP(30);
-        }
+      tree.backup(r, c, s, rs, ho.value, ho.reward, ho.pp);
+      MZH_STAMP(22);
+      if (s + 1 < S) {
+        group_sync();
+        tree.select(r, c, s + 1, rs);
+        MZH_STAMP(30);
       }
     }
     __syncthreads();
@@ -164,6 +166,8 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
   }
 
   // ---------------- results (mcts.py:111-126, 154-176) ----------------
+  if (town && tc == 0) rs.store(st, tr);
+  __syncthreads();
   if (tid < R * 8) {
     const int r = tid >> 3, c = tid & 7;
     if (r < nvalid && c == 0) tree.results(r);

@@ -133,6 +133,48 @@ __device__ __forceinline__ double mzh_pow(double x, double e) {
 }
 
 
+// A root's search state between the tree steps, held in registers by every lane of its 8-lane group
+// (all values group-uniform; rootW is kept by lane 0, which runs the value chain).  The LDS copy
+// (SearchSmem) is read once before the first selection and written back once for the results.
+struct MzhRootReg {
+  double mmax, mmin, den, dinv;  // MinMaxStats + normaliser (mzh_mm_set)
+  double rootW;
+  int rootN, firstTie, extra, tie, steps;
+  int depth, leafE, leafA;  // the current simulation's leaf (select -> backup)
+  __device__ __forceinline__ void set_mm(double mx, double mn) {
+    mmax = mx;
+    mmin = mn;
+    den = mx - mn;
+    dinv = mx > mn ? 1.0 / (mx - mn) : 0.0;
+  }
+  template <int R, int DC>
+  __device__ __forceinline__ void load(const SearchSmem<R, DC>& st, int r) {
+    mmax = st.mm[r][0];
+    mmin = st.mm[r][1];
+    den = st.mm[r][2];
+    dinv = st.mm[r][3];
+    rootW = st.rootW[r];
+    rootN = st.rootN[r];
+    firstTie = st.firstTie[r];
+    extra = st.extra[r];
+    tie = st.tie[r];
+    steps = st.steps[r];
+    depth = st.depth[r];
+    leafE = 0;
+    leafA = 0;
+  }
+  template <int R, int DC>
+  __device__ __forceinline__ void store(SearchSmem<R, DC>& st, int r) const {
+    mzh_mm_set(st.mm[r], mmax, mmin);
+    st.rootW[r] = rootW;
+    st.rootN[r] = rootN;
+    st.firstTie[r] = firstTie;
+    st.extra[r] = extra;
+    st.steps[r] = steps;
+    st.depth[r] = depth;
+  }
+};
+
 // Per-root steps over one workgroup's trees.  R roots (st / sm rows 0..R-1), DC path depths cached
 // in LDS, `path` = [R][S + 1] selection slots.  SM: the MLP storage holding each root's row of the
 // MLP input / output (x, act, pi, value, reward).
@@ -148,13 +190,13 @@ struct MzhTree {
   double disc;
   bool noised;
 
-  __device__ __forceinline__ void select(const int r, const int c, const int s) {
+  __device__ __forceinline__ void select(const int r, const int c, const int s, MzhRootReg& rs) {
     const MzhBlock* tb = reinterpret_cast<const MzhBlock*>(p.tree) + (size_t)(root0 + r) * p.E;
-    const double mmax = st.mm[r][0], mmin = st.mm[r][1], den = st.mm[r][2], dinv = st.mm[r][3];
+    const double mmax = rs.mmax, mmin = rs.mmin, den = rs.den, dinv = rs.dinv;
     const bool has = mmax > mmin;
-    int firstTie = st.firstTie[r];
-    int extra = st.extra[r];
-    const int tie = st.tie[r];
+    int firstTie = rs.firstTie;
+    int extra = rs.extra;
+    const int tie = rs.tie;
     MZH_STAMP_DECL
 #ifdef MZH_STAMPS
     asm volatile("" ::"v"(tie), "v"(dinv));
@@ -171,7 +213,7 @@ struct MzhTree {
       Xc = rb.X[c];
       Wc = rb.W[c];
       Rc = rb.R[c];
-      const float u = mzh_ucb(Nc, Wc, Rc, rb.P64[c], noised || p.np1, table[st.rootN[r]], disc, has, mmin, den, dinv, inv);
+      const float u = mzh_ucb(Nc, Wc, Rc, rb.P64[c], noised || p.np1, table[rs.rootN], disc, has, mmin, den, dinv, inv);
       ucb = c < MZH_A ? u : -__builtin_inff();
     }
     int pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
@@ -245,14 +287,12 @@ struct MzhTree {
     }
     MZH_LSTAMP_FLUSH(24);
     MZH_STAMP(15);
-    if (c == 0) {
-      st.depth[r] = depth;
-      st.leafE[r] = e;
-      st.leafA[r] = pick;
-      st.steps[r] += depth;
-      st.firstTie[r] = firstTie;
-      st.extra[r] = extra;
-    }
+    rs.depth = depth;
+    rs.leafE = e;
+    rs.leafA = pick;
+    rs.steps += depth;
+    rs.firstTie = firstTie;
+    rs.extra = extra;
     if (!REPLAY) {
       // MLP input: the leaf's parent latent (mcts.py:89-92).  The node expanded by the previous
       // simulation (index s; the root at s = 0) is still in sm.x as that MLP's output.
@@ -275,7 +315,9 @@ struct MzhTree {
   // Lane 0 of the root's group runs the value chain leaf -> root (two fp64 ops per level, the only
   // serial part); the 8 lanes then update the cached path nodes in parallel and reduce the
   // MinMaxStats candidates (max/min are exact and order-free).
-  __device__ __forceinline__ void backup(const int r, const int c, const int s) {
+  // val / rew: the new node's value and reward (every lane), pp: lane c's child prior
+  __device__ __forceinline__ void backup(const int r, const int c, const int s, MzhRootReg& rs, float val, float rew,
+                                         float pp) {
     MzhBlock* tb = reinterpret_cast<MzhBlock*>(p.tree) + (size_t)(root0 + r) * p.E;
     MzhRootBlk& rb = st.root[r];
     const int enew = s + 1;
@@ -293,12 +335,11 @@ struct MzhTree {
     if (c < MZH_A) {
       *reinterpret_cast<uint32_t*>(&nb->sl[c].nx) = 0xFFFF0000u;  // N = 0, X = -1
       nb->sl[c].R = 0.0f;
-      nb->sl[c].P = sm.pi[r * 8 + c];
+      nb->sl[c].P = pp;
       nb->W[c] = 0.0;
     }
     MZH_STAMP(16);
-    const int le = st.leafE[r], la = st.leafA[r], depth = st.depth[r];
-    const float rew = sm.reward[r];
+    const int le = rs.leafE, la = rs.leafA, depth = rs.depth;
     double lmax = -__builtin_inf(), lmin = __builtin_inf();
     if (c == 0) {
       if (le == 0) {
@@ -308,7 +349,7 @@ struct MzhTree {
         tb[le].sl[la].nx.X = (int16_t)enew;
         tb[le].sl[la].R = rew;
       }
-      double v = (double)sm.value[r];
+      double v = (double)val;
       int j = depth - 1;
       for (; j >= DC; --j) {  // beyond the LDS path cache (rare): update here from HBM
         const int slot = path[r * PL + j];
@@ -339,10 +380,9 @@ struct MzhTree {
         const double vn = rw + disc * v;
         v = jj <= jtop ? vn : v;
       }
-      const double W = st.rootW[r] + v;
-      const int N = st.rootN[r] + 1;
-      st.rootW[r] = W;
-      st.rootN[r] = N;
+      const double W = rs.rootW + v;
+      const int N = rs.rootN + 1;
+      rs.rootW = W;
       const double q = 0.0 + disc * mzh_div(W, (double)N, inv[N]);  // root rwd = 0.0
       lmax = q > lmax ? q : lmax;
       lmin = q < lmin ? q : lmin;
@@ -371,11 +411,9 @@ struct MzhTree {
       lmin = q < lmin ? q : lmin;
     }
     MZH_STAMP(18);
+    rs.rootN += 1;
     mzh_maxmin8d(lmax, lmin);
-    if (c == 0) {
-      const double mx = st.mm[r][0], mn = st.mm[r][1];
-      mzh_mm_set(st.mm[r], lmax > mx ? lmax : mx, lmin < mn ? lmin : mn);
-    }
+    rs.set_mm(lmax > rs.mmax ? lmax : rs.mmax, lmin < rs.mmin ? lmin : rs.mmin);
     MZH_STAMP(29);
   }
 
