@@ -89,6 +89,25 @@ __device__ __forceinline__ float mzh_expf(float x) {
   return p * __int_as_float((ni + 127) << 23);
 }
 
+// mzh_expf for x <= 0 (softmax arguments l - max): the overflow branch dropped
+__device__ __forceinline__ float mzh_expf_np(float x) {
+  if (x < -87.0f) return 0.0f;
+  float n = __builtin_rintf(x * 1.44269502162933349609375f);
+  float r = __builtin_fmaf(n, -0.693359375f, x);
+  r = __builtin_fmaf(n, 2.12194440e-4f, r);
+  float p = 1.9875691500e-4f;
+  p = __builtin_fmaf(p, r, 1.3981999507e-3f);
+  p = __builtin_fmaf(p, r, 8.3334519073e-3f);
+  p = __builtin_fmaf(p, r, 4.1665795894e-2f);
+  p = __builtin_fmaf(p, r, 1.6666665459e-1f);
+  p = __builtin_fmaf(p, r, 5.0000001201e-1f);
+  float r2 = r * r;
+  p = __builtin_fmaf(p, r2, r);
+  p = p + 1.0f;
+  int ni = (int)n;
+  return p * __int_as_float((ni + 127) << 23);
+}
+
 // _signed_parabolic (networks.py:186-189)
 __device__ __forceinline__ float mzh_signed_parabolic(float x) {
   float a = __builtin_fabsf(x);
@@ -623,11 +642,18 @@ __device__ __forceinline__ MzhHeadOut mzh_heads_row(SM& sm, int row, int q, int 
   const float mp = mzh_max8(lg);
 #pragma unroll
   for (int h = 0; h < 2; ++h) m[h] = mzh_max8(m[h]);
-  const float ep = q < MZH_A ? mzh_expf(lg - mp) : 0.0f;
+  // every exponent argument is <= 0; xmin tracks the smallest one that feeds a probability
+  const float xp = lg - mp;
+  const float ep = q < MZH_A ? mzh_expf_np(xp) : 0.0f;
+  float xmin = q < MZH_A ? xp : 0.0f;
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int i = 0; i < 5; ++i) e[h][i] = (q + 8 * i < 33) ? mzh_expf(e[h][i] - m[h]) : 0.0f;
+    for (int i = 0; i < 5; ++i) {
+      const float xv = e[h][i] - m[h];
+      e[h][i] = (q + 8 * i < 33) ? mzh_expf_np(xv) : 0.0f;
+      if (h < nh && q + 8 * i < 33) xmin = xv < xmin ? xv : xmin;
+    }
   float sh[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -640,16 +666,24 @@ __device__ __forceinline__ MzhHeadOut mzh_heads_row(SM& sm, int row, int q, int 
   const float sp = mzh_sum8(ep);
 #pragma unroll
   for (int h = 0; h < 2; ++h) sh[h] = mzh_sum8(sh[h]);
-  // probabilities: Markstein division from one reciprocal per head, IEEE fallback when flagged
-  bool slow = false;
+  // probabilities: Markstein division from one reciprocal per head, IEEE fallback when flagged.
+  // The sums lie in [1, 33], so with every argument >= -65 each numerator is 0 or >= e^-65 and each
+  // quotient >= e^-65 / 33 > 2^-100: the residual stays normal and the quotient is RN(a / s) (the
+  // condition mzh_fdiv checks per division, decided here once per lane from the arguments)
+  const bool slow = xmin < -65.0f;
   float pk[2][5];
   const float yp = 1.0f / sp;
-  float pp = mzh_fdiv(ep, sp, yp, slow);
+  auto mdiv = [](float a, float b, float y) {
+    const float qq = a * y;
+    const float rr = __builtin_fmaf(-qq, b, a);
+    return __builtin_fmaf(rr, y, qq);
+  };
+  float pp = mdiv(ep, sp, yp);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const float y = 1.0f / sh[h];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) pk[h][i] = mzh_fdiv(e[h][i], sh[h], y, slow);
+    for (int i = 0; i < 5; ++i) pk[h][i] = mdiv(e[h][i], sh[h], y);
   }
   if (__builtin_expect(__ballot(slow) != 0, 0)) {
     pp = ep / sp;
