@@ -457,7 +457,9 @@ __device__ __forceinline__ void mzh_fetch(floatx4* f, float* bv, const MzhChunk&
 template <int MT, int NJ, int KB, bool ALL = false, int PT = 0, int PNB = 0, bool NAT = false>
 __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhChunk& c, const float* A, int lda,
                                               bool relu, const float* oht, const int* act, int lane,
-                                              const MzhChunk* pc = nullptr) {
+                                              const MzhChunk* pc = nullptr, const floatx4* areg = nullptr) {
+  // areg (optional): the A operand of all KB k-blocks already in registers, [kb * MT + m] (chunks
+  // of one phase that share A load it once)
   static_assert(PT <= 16 && PNB <= 4, "ring chunk too large");
   const int r = lane & 15, g = lane >> 4;
   const float4* pw = PT > 0 ? pc->w[0] : nullptr;
@@ -477,8 +479,11 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
   // between its MFMAs
   floatx4 a[2][MT];  // [buffer][row tile]: k-steps j = 0..3 of one k-block (A in k-block order)
   const float* arow = A + r * lda + 4 * g;
+  if (!areg) {
 #pragma unroll
-  for (int m = 0; m < MT; ++m) a[0][m] = *reinterpret_cast<const floatx4*>(arow + m * 16 * lda);
+    for (int m = 0; m < MT; ++m) a[0][m] = *reinterpret_cast<const floatx4*>(arow + m * 16 * lda);
+  }
+  auto aop = [&](int kb, int m) -> const floatx4& { return areg ? areg[kb * MT + m] : a[kb & 1][m]; };
   float oh[NJ * MT * 4];
   if (oht) {
     __builtin_amdgcn_sched_barrier(0);
@@ -511,7 +516,7 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
   };
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
-    if (kb + 1 < KB) {
+    if (kb + 1 < KB && !areg) {
 #pragma unroll
       for (int m = 0; m < MT; ++m)
         a[(kb + 1) & 1][m] = *reinterpret_cast<const floatx4*>(arow + m * 16 * lda + (kb + 1) * 16);
@@ -525,7 +530,7 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
           if (ALL || q < c.nj) {
 #pragma unroll
             for (int m = 0; m < MT; ++m)
-              acc[q][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kb & 1][m][j], f[q * KB + kb][j], acc[q][m], 0, 0, 0);
+              acc[q][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(aop(kb, m)[j], f[q * KB + kb][j], acc[q][m], 0, 0, 0);
           }
         }
       }
@@ -540,7 +545,7 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
           for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int m = 0; m < MT; ++m)
-              acc[q][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kb & 1][m][j], f[q * KB + kb][j], acc[q][m], 0, 0, 0);
+              acc[q][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(aop(kb, m)[j], f[q * KB + kb][j], acc[q][m], 0, 0, 0);
         }
         if (q * KB + kb < PT) refill(q * KB + kb);
         epilogue(q);
@@ -860,6 +865,16 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
   bar();
   MZH_STAMP(7);
   {
+    // the prediction chunks of this phase (P1, P2, P3) all read the normalised latent sm.x: its four
+    // k-blocks are loaded into registers once
+    floatx4 ax[4 * MT];
+    {
+      const float* arow = sm.x + (lane & 15) * MZH_LD64 + 4 * (lane >> 4);
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) ax[kb * MT + m] = *reinterpret_cast<const floatx4*>(arow + m * 16 * MZH_LD64 + kb * 16);
+    }
     const MzhChunk c_p3 = mzh_pred_tiles<R>(sm, net, P3, N2);
     if (r2)
       mzh_mma_store<MT, 1, 16, true, 4 * N2, N2, true>(fb, bb, mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP),
@@ -867,19 +882,19 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
                                                        &c_p3);  // rwd2 -> reward logits
     else
       mzh_mma_store<MT, 4, 4, true, 4 * N2, N2>(fb, bb, mzh_pred_tiles<R>(sm, net, P1, 4), sm.x, MZH_LD64, true,
-                                                nullptr, nullptr, lane, &c_p3);
+                                                nullptr, nullptr, lane, &c_p3, ax);
     MZH_STAMP(8);
     if (ht) {
       const MzhChunk c_h = mzh_head_chunk<R>(sm, net, wave);
-      mzh_mma_store<MT, 4, 4, true, 16, 1>(fa, ba, c_p2, sm.x, MZH_LD64, true, nullptr, nullptr, lane, &c_h);
+      mzh_mma_store<MT, 4, 4, true, 16, 1>(fa, ba, c_p2, sm.x, MZH_LD64, true, nullptr, nullptr, lane, &c_h, ax);
     } else {
-      mzh_mma_store<MT, 4, 4, true>(fa, ba, c_p2, sm.x, MZH_LD64, true, nullptr, nullptr, lane);
+      mzh_mma_store<MT, 4, 4, true>(fa, ba, c_p2, sm.x, MZH_LD64, true, nullptr, nullptr, lane, nullptr, ax);
     }
     if (NEXT) {
       const MzhChunk c_n2 = mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64);
-      mzh_mma_store<MT, N2, 4, true, 16, 1>(fb, bb, c_p3, sm.x, MZH_LD64, true, nullptr, nullptr, lane, &c_n2);
+      mzh_mma_store<MT, N2, 4, true, 16, 1>(fb, bb, c_p3, sm.x, MZH_LD64, true, nullptr, nullptr, lane, &c_n2, ax);
     } else {
-      mzh_mma_store<MT, N2, 4, true>(fb, bb, c_p3, sm.x, MZH_LD64, true, nullptr, nullptr, lane);
+      mzh_mma_store<MT, N2, 4, true>(fb, bb, c_p3, sm.x, MZH_LD64, true, nullptr, nullptr, lane, nullptr, ax);
     }
   }
   MZH_STAMP(9);
