@@ -508,6 +508,11 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
       ws.pcR[0][rho] = ws.rR[pick][rho];
       ws.pcN[0][rho] = Np;
       int e = 0, d = 1;
+      // 16-root waves (NT = 1) prefetch the children's blocks one level ahead (16,384 roots: 2.66 ->
+      // 2.57 ms); at 32 roots per wave the partner wave's MFMA stream already covers the latency
+      // (65,536 roots: neutral), so NT = 2 leaves the load queue to the block loads
+      constexpr bool kPF = NT == 1;
+      int pf0 = 0, pf1 = 0, pf2 = 0;
       while (X >= 0 && d <= S) {  // depth <= s + 1 always; the bound only guards against a corrupt tree
         e = X;
         const int4* bp = reinterpret_cast<const int4*>(&tb[e]);
@@ -519,6 +524,15 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
           dw[4 * k + 1] = q.y;
           dw[4 * k + 2] = q.z;
           dw[4 * k + 3] = q.w;
+        }
+        if (kPF) {
+          // retire the previous level's child prefetches (older than this block's loads), then
+          // touch this lane's three children's blocks: the next level's block is one of them
+          asm volatile("" ::"v"(pf0), "v"(pf1), "v"(pf2));
+          const int x0 = (half ? dw[3] : dw[0]) >> 16, x1 = (half ? dw[4] : dw[1]) >> 16, x2 = (half ? dw[5] : dw[2]) >> 16;
+          pf0 = *reinterpret_cast<const int*>(&tb[x0 >= 0 ? x0 : e]);
+          pf1 = *reinterpret_cast<const int*>(&tb[x1 >= 0 ? x1 : e]);
+          pf2 = *reinterpret_cast<const int*>(&tb[x2 >= 0 ? x2 : e]);
         }
         double Wc[6];
         float Rc[6];
@@ -561,6 +575,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
         }
         ++d;
       }
+      if (kPF) asm volatile("" ::"v"(pf0), "v"(pf1), "v"(pf2));
       depth = d;
       leafE = e;
       leafA = pick;
