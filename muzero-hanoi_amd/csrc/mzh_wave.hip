@@ -15,8 +15,8 @@
 //
 // Schedule variants measured and not shipped (numbers in DESIGN.md §6/§8): an explicit ping-pong of
 // the two waves per SIMD, software-pipelined MLP chains, LDS parking of the tree statistics,
-// laundered weight pointers, cached child values in the tree block, child-block prefetch in
-// selection, a register reciprocal.
+// laundered weight pointers, cached child values in the tree block, a register reciprocal.  The
+// child-block prefetch in selection is shipped for 16-root waves only (neutral at 32 roots per wave).
 //
 // Reference: MCTS/mcts.py:34-126 (run_mcts), MCTS/node.py:30-136 (expand/backup/best_child),
 // MCTS/utils_mcts.py:1-16 (MinMaxStats), networks.py:71-196 (initial/recurrent inference).
