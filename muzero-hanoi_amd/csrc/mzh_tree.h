@@ -112,7 +112,8 @@ __device__ __forceinline__ void mzh_mm_set(double* mm, double mx, double mn) {
 // of the group returns the same pick.
 __device__ __forceinline__ int mzh_group_pick(float ucb, int c, int lane, int tie, int& firstTie, int& extra) {
   const float m = mzh_max8_nonan(ucb);
-  const unsigned long long bal = __ballot(c < MZH_A && ucb == m);
+  (void)c;  // lanes 6, 7 carry -inf, never the group maximum (the UCBs are finite)
+  const unsigned long long bal = __builtin_amdgcn_ballot_w64(ucb == m);
   const unsigned mask = (unsigned)(bal >> (lane & ~7)) & 0x3Fu;
   const int cnt = __popc(mask);
   const int first = __ffs(mask) - 1;
