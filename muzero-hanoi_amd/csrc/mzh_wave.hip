@@ -515,53 +515,106 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
       int pf0 = 0, pf1 = 0, pf2 = 0;
       while (X >= 0 && d <= S) {  // depth <= s + 1 always; the bound only guards against a corrupt tree
         e = X;
-        const int4* bp = reinterpret_cast<const int4*>(&tb[e]);
-        int dw[32];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int4 q = bp[k];
-          dw[4 * k] = q.x;
-          dw[4 * k + 1] = q.y;
-          dw[4 * k + 2] = q.z;
-          dw[4 * k + 3] = q.w;
-        }
-        if (kPF) {
-          // retire the previous level's child prefetches (older than this block's loads), then
-          // touch this lane's three children's blocks: the next level's block is one of them
-          asm volatile("" ::"v"(pf0), "v"(pf1), "v"(pf2));
-          const int x0 = (half ? dw[3] : dw[0]) >> 16, x1 = (half ? dw[4] : dw[1]) >> 16, x2 = (half ? dw[5] : dw[2]) >> 16;
-          pf0 = *reinterpret_cast<const int*>(&tb[x0 >= 0 ? x0 : e]);
-          pf1 = *reinterpret_cast<const int*>(&tb[x1 >= 0 ? x1 : e]);
-          pf2 = *reinterpret_cast<const int*>(&tb[x2 >= 0 ? x2 : e]);
-        }
-        double Wc[6];
-        float Rc[6];
-#pragma unroll
-        for (int c = 0; c < MZH_A; ++c) {
-          Rc[c] = __int_as_float(dw[6 + c]);
-          Wc[c] = __hiloint2double(dw[19 + 2 * c], dw[18 + 2 * c]);
-        }
-        const double tn = table[Np];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          // this lane's three children (dw is the whole block on both lanes)
-          const int nxj = half ? dw[3 + j] : dw[j];
-          const float Rj = half ? Rc[3 + j] : Rc[j];
-          const double Wj = half ? Wc[3 + j] : Wc[j];
-          const float Pj = __int_as_float(half ? dw[15 + j] : dw[12 + j]);
-          u[j] = mzw_ucb(nxj & 0xFFFF, Wj, Rj, (double)Pj, p.np1, tn, disc, has, mmin, den, dinv, inv);
-        }
-        pick = mzw_pick_pair(u, half, tie, firstTie, extra);
-        int nx = dw[0];
-        double Wp = Wc[0];
-        float Rp = Rc[0];
-#pragma unroll
-        for (int c = 1; c < MZH_A; ++c)
-          if (pick == c) {
-            nx = dw[c];
-            Wp = Wc[c];
-            Rp = Rc[c];
+        int nx;
+        double Wp;
+        float Rp;
+        if constexpr (NT == 1) {
+          // 16-root waves: this lane's half of the block only -- its three children's N|X, R, P and
+          // W (5 loads, 60 B, instead of the whole 128-B line on both lanes); the picked child's
+          // fields come from the lane that holds them over v_permlane32_swap (16,384 roots -1.4%;
+          // at 32 roots per wave the extra registers spill: +1.6%, so NT = 2 loads the line)
+          const unsigned char* blk = reinterpret_cast<const unsigned char*>(&tb[e]);
+          const uint3 hnx = *reinterpret_cast<const uint3*>(blk + 12 * half);
+          const uint3 hR = *reinterpret_cast<const uint3*>(blk + 24 + 12 * half);
+          const uint3 hP = *reinterpret_cast<const uint3*>(blk + 48 + 12 * half);
+          const uint4 hW01 = *reinterpret_cast<const uint4*>(blk + 72 + 24 * half);
+          const uint2 hW2 = *reinterpret_cast<const uint2*>(blk + 88 + 24 * half);
+          const int hn[3] = {(int)hnx.x, (int)hnx.y, (int)hnx.z};
+          const float hr[3] = {__uint_as_float(hR.x), __uint_as_float(hR.y), __uint_as_float(hR.z)};
+          const float hp[3] = {__uint_as_float(hP.x), __uint_as_float(hP.y), __uint_as_float(hP.z)};
+          const double hw[3] = {__hiloint2double((int)hW01.y, (int)hW01.x), __hiloint2double((int)hW01.w, (int)hW01.z),
+                                __hiloint2double((int)hW2.y, (int)hW2.x)};
+          if (kPF) {
+            asm volatile("" ::"v"(pf0), "v"(pf1), "v"(pf2));
+            const int x0 = hn[0] >> 16, x1 = hn[1] >> 16, x2 = hn[2] >> 16;
+            pf0 = *reinterpret_cast<const int*>(&tb[x0 >= 0 ? x0 : e]);
+            pf1 = *reinterpret_cast<const int*>(&tb[x1 >= 0 ? x1 : e]);
+            pf2 = *reinterpret_cast<const int*>(&tb[x2 >= 0 ? x2 : e]);
           }
+          const double tn = table[Np];
+  #pragma unroll
+          for (int j = 0; j < 3; ++j) u[j] = mzw_ucb(hn[j] & 0xFFFF, hw[j], hr[j], (double)hp[j], p.np1, tn, disc, has, mmin, den, dinv, inv);
+          pick = mzw_pick_pair(u, half, tie, firstTie, extra);
+          // this lane's candidate for the picked slot (valid on the owning half), then the owner's copy
+          const int jl = pick - 3 * half;
+          int cn = hn[0];
+          float cr = hr[0];
+          double cw = hw[0];
+  #pragma unroll
+          for (int q = 1; q < 3; ++q)
+            if (jl == q) {
+              cn = hn[q];
+              cr = hr[q];
+              cw = hw[q];
+            }
+          auto take = [&](unsigned v) {
+            const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+            // r = {lanes 0-31 value, lanes 32-63 value} on both lanes of the pair
+            return pick >= 3 ? r[1] : r[0];
+          };
+          nx = (int)take((unsigned)cn);
+          Rp = __uint_as_float(take(__float_as_uint(cr)));
+          const long long wb = __double_as_longlong(cw);
+          Wp = __hiloint2double((int)take((unsigned)(wb >> 32)), (int)take((unsigned)(wb & 0xFFFFFFFFll)));
+        } else {
+          const int4* bp = reinterpret_cast<const int4*>(&tb[e]);
+          int dw[32];
+  #pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int4 q = bp[k];
+            dw[4 * k] = q.x;
+            dw[4 * k + 1] = q.y;
+            dw[4 * k + 2] = q.z;
+            dw[4 * k + 3] = q.w;
+          }
+          if (kPF) {
+            // retire the previous level's child prefetches (older than this block's loads), then
+            // touch this lane's three children's blocks: the next level's block is one of them
+            asm volatile("" ::"v"(pf0), "v"(pf1), "v"(pf2));
+            const int x0 = (half ? dw[3] : dw[0]) >> 16, x1 = (half ? dw[4] : dw[1]) >> 16, x2 = (half ? dw[5] : dw[2]) >> 16;
+            pf0 = *reinterpret_cast<const int*>(&tb[x0 >= 0 ? x0 : e]);
+            pf1 = *reinterpret_cast<const int*>(&tb[x1 >= 0 ? x1 : e]);
+            pf2 = *reinterpret_cast<const int*>(&tb[x2 >= 0 ? x2 : e]);
+          }
+          double Wc[6];
+          float Rc[6];
+  #pragma unroll
+          for (int c = 0; c < MZH_A; ++c) {
+            Rc[c] = __int_as_float(dw[6 + c]);
+            Wc[c] = __hiloint2double(dw[19 + 2 * c], dw[18 + 2 * c]);
+          }
+          const double tn = table[Np];
+  #pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            // this lane's three children (dw is the whole block on both lanes)
+            const int nxj = half ? dw[3 + j] : dw[j];
+            const float Rj = half ? Rc[3 + j] : Rc[j];
+            const double Wj = half ? Wc[3 + j] : Wc[j];
+            const float Pj = __int_as_float(half ? dw[15 + j] : dw[12 + j]);
+            u[j] = mzw_ucb(nxj & 0xFFFF, Wj, Rj, (double)Pj, p.np1, tn, disc, has, mmin, den, dinv, inv);
+          }
+          pick = mzw_pick_pair(u, half, tie, firstTie, extra);
+          nx = dw[0];
+          Wp = Wc[0];
+          Rp = Rc[0];
+  #pragma unroll
+          for (int c = 1; c < MZH_A; ++c)
+            if (pick == c) {
+              nx = dw[c];
+              Wp = Wc[c];
+              Rp = Rc[c];
+            }
+        }
         Np = nx & 0xFFFF;
         X = nx >> 16;
         const uint16_t slot = (uint16_t)(e * 8 + pick);
