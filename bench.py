@@ -12,8 +12,8 @@ over the ranks); `--roots-per-gpu B` runs B roots on every GPU (weak scaling, la
 MuZeroNet(TD_return=True) with random-init weights (torch.manual_seed(0), broadcast once),
 training-like search parameters (gamma 0.8, Dirichlet alpha 0.25 / eps 0.25, T=1, stochastic).
 One step = one mzh_search launch over every root on the rank (root inference + S x {select, MFMA
-MLP, backup} + play policy), followed by the RCCL all_gather of the visit histograms
-(north_star's only exchange).  Inputs are resident in HBM before timing starts.
+MLP, backup} + play policy), followed by one RCCL all_gather of every root's result (visit
+histogram, action, fp64 root Q: what run_mcts returns; north_star's only exchange).  Inputs are resident in HBM before timing starts.
 
 Rank 0 prints ONE JSON line (contract in the task statement) including
   roofline        the fused search kernel (fp32-MFMA bound; achieved = algorithmic matmul FLOPs per
@@ -84,7 +84,7 @@ def parse():
                    help="nccl (= RCCL, one rank per GPU); gloo lets ranks share a GPU to rehearse the N>1 path")
     p.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     p.add_argument("--cpu-baseline-procs", type=int, default=0,
-                   help="0: one process per available host core (capped at 16, the GPU box's CPU share)")
+                   help="0: one process per physical core, capped at the GPU box's 16-CPU share per job")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return p.parse_args()
@@ -138,24 +138,54 @@ def _cpu_model():
     return "unknown"
 
 
+def _physical_cores(cpus):
+    """distinct (package, core) pairs among the logical CPUs `cpus` (SMT siblings counted once)"""
+    seen = set()
+    for c in cpus:
+        base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+        try:
+            seen.add((open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip()))
+        except OSError:
+            seen.add(("?", str(c)))
+    return len(seen)
+
+
+# the GPU box grants one job a 16-CPU share of its host (os.cpu_count() shows the whole machine): the
+# measured pool stays within it; the all-physical-core figure BASELINE.md 3 names is reported beside
+# it as the single-process rate x the physical cores (linear scaling, an upper bound)
+CPU_SHARE = 16
+
+
 def cpu_baseline(n_disks, S, seconds, seed, procs=0):
-    """One process per host core (torch.set_num_threads(1) each, roots partitioned round-robin),
-    aggregate sims/s = all processes' sims / the slowest process's wall time; plus the 1-process
-    figure from a separate single-process run of the same length."""
+    """One process per core of the job's CPU share (torch.set_num_threads(1) each, roots partitioned
+    round-robin), aggregate sims/s = all processes' sims / the slowest process's wall time; plus the
+    1-process figure from a separate single-process run, and that figure scaled to every physical
+    core of the affinity set (BASELINE.md 3's "one process per physical host core"), labelled as an
+    extrapolation."""
     import multiprocessing as mp
 
-    avail = len(os.sched_getaffinity(0))
-    P = procs if procs > 0 else min(avail, 16)
+    aff = sorted(os.sched_getaffinity(0))
+    avail = len(aff)
+    phys = _physical_cores(aff)
+    P = procs if procs > 0 else min(phys, CPU_SHARE)
     ctx = mp.get_context("spawn")  # fresh interpreters; this process has not touched the GPU
     single_roots, single_dt = _cpu_worker((n_disks, S, seconds / 3, seed, 0, 1))
     with ctx.Pool(P) as pool:
         res = pool.map(_cpu_worker, [(n_disks, S, seconds, seed, k, P) for k in range(P)])
     roots = sum(r for r, _ in res)
     dt = max(t for _, t in res)
+    single = single_roots * S / single_dt
     return {"value": roots * S / dt, "unit": "sims/s", "cores": P, "kind": "port",
-            "cpu_model": _cpu_model(), "cores_available": avail,
-            "single_core_value": single_roots * S / single_dt,
-            "sample": f"{P} processes x {seconds:.0f} s (one per host core, torch threads=1 each): {roots} roots x "
+            "cpu_model": _cpu_model(), "cores_available": avail, "physical_cores_available": phys,
+            "single_core_value": single,
+            "all_physical_cores": {"value": single * phys, "cores": phys, "measured": False,
+                                   "what": f"single_core_value x {phys} physical cores of the affinity set "
+                                           f"(BASELINE.md 3: one process per physical host core), linear scaling "
+                                           f"assumed -- an upper bound; not measured because the GPU box grants "
+                                           f"this job a {CPU_SHARE}-CPU share and a {phys}-process pool would "
+                                           f"oversubscribe it (the measured {P}-process value scales "
+                                           f"{roots * S / dt / max(single, 1e-9):.1f}x over one process)"},
+            "sample": f"{P} processes x {seconds:.0f} s (one per core of the job's CPU share, torch threads=1 each): {roots} roots x "
                       f"{S} sims, {n_disks}-disk, fresh MCTS per root, T=1 stochastic, roots partitioned "
                       f"round-robin; single_core_value: 1 process, {single_roots} roots in {single_dt:.1f} s. "
                       f"oracle/py_port.py restates MCTS/mcts.py + networks.py and matches the reference's "
@@ -208,6 +238,42 @@ def tree_bytes(sel_steps_sum, n_roots, S, expand_bytes):
     return SEL_BYTES * sel_steps_sum + BACKUP_BYTES * (sel_steps_sum + n_roots * S) + expand_bytes * n_roots * S
 
 
+def traffic_key(n_disks, S, B, kern="auto"):
+    """the key of one bench workload in profiles/traffic_latest.json (tools/traffic.py writes it
+    from the same function): disks, sims, roots on this GPU and the kernel that serves them"""
+    return f"hanoi{n_disks}_s{S}_roots{B}_{kernel_name(kern, B)[0]}"
+
+
+def workload_shape(config, world=1, rank=0, roots_per_gpu=None, disks=None, sims=None):
+    """(disks, sims, roots on this rank, global roots) of a bench invocation"""
+    from muzero_hanoi_amd import distributed as mdist
+
+    N, GB, S, _ = CONFIGS[config]
+    N, S = disks or N, sims or S
+    if roots_per_gpu is not None:
+        GB = world * roots_per_gpu
+    s0, s1 = mdist.shard_range(GB, world, rank)
+    return N, S, s1 - s0, GB
+
+
+def lookup_traffic(path, key):
+    """(entry, note): the PMC-counted HBM bytes of this workload if profiled on THIS build"""
+    if not os.path.exists(path):
+        return None, "no traffic file"
+    try:
+        entries = json.load(open(path)).get("entries", {})
+    except Exception as e:  # noqa: BLE001
+        return None, f"unreadable traffic file: {e}"
+    ent = entries.get(key)
+    if ent is None:
+        return None, f"workload {key} not profiled"
+    from muzero_hanoi_amd import _lib
+
+    if ent.get("build_id") != _lib.build_id():
+        return None, f"profiled on build {ent.get('build_id')}, not this build {_lib.build_id()}"
+    return ent, "rocprofv3 PMC of this build (tools/prof.sh + tools/traffic.py)"
+
+
 def kernel_name(kern, B):
     """the search kernel mzh_api.hip choose_kernel() / pick_tile() launches for B roots"""
     kern_sel = kern if kern != "auto" else ("wave" if B >= 53248 else "wave16" if B > 8192 else "coop")
@@ -250,6 +316,7 @@ def main():
         else:
             dist.init_process_group(a.dist_backend)
 
+    from muzero_hanoi_amd import _lib
     from muzero_hanoi_amd import distributed as mdist
     from muzero_hanoi_amd import engine, rng
     from muzero_hanoi_amd.networks import MuZeroNet
@@ -281,7 +348,7 @@ def main():
     for _ in range(a.warmup):
         search()
         if gather:
-            mdist.gather_visits(out["visits"], GB, world)
+            mdist.gather_results(out, GB, world)
     torch.cuda.synchronize(dev)
     # correctness sanity on the warmed-up result (outside timing)
     vis = out["visits"]
@@ -299,7 +366,7 @@ def main():
         search()
         evs[k][1].record(stream)
         if gather:
-            mdist.gather_visits(out["visits"], GB, world)
+            mdist.gather_results(out, GB, world)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -361,16 +428,11 @@ def main():
     # the cooperative kernel one 4-wave workgroup per CU
     nt = 2 if kname.startswith("mzh_wave_kernel<2") else 1 if kname.startswith("mzh_wave_kernel<1") else 0
     wps = 1 if nt == 0 else min(2, max(1, -(-B // (16 * nt * 1024))))
-    traffic = None
-    if os.path.exists(a.traffic_json):
-        try:
-            tj = json.load(open(a.traffic_json))
-            if tj.get("workload") == f"hanoi{N}_s{S}_roots{B}":
-                traffic = tj.get("hbm_bytes_per_launch")
-                if tree is not None:
-                    tree["traffic"] = tj.get("tree_hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    tkey = traffic_key(N, S, B, a.kernel)
+    tent, tnote = lookup_traffic(a.traffic_json, tkey)
+    traffic = tent.get("hbm_bytes_per_launch") if tent else None
+    if tree is not None and tent:
+        tree["traffic"] = tent.get("tree_hbm_bytes_per_launch")
 
     if weak:
         workload = (f"weak scaling: {N}-disk, {B} roots per GPU ({GB} over {world} GPUs), {S} sims/move "
@@ -393,9 +455,11 @@ def main():
         "data": f"synthetic: uniform random non-goal {N}-disk root states, random-init MuZeroNet(TD_return=True)",
         "config": {"workload": workload, "baseline_config": None if weak else a.config, "n_disks": N,
                    "sims_per_move": S, "roots_per_gpu": B, "global_roots": GB,
-                   "parallelism": f"dp{world} (independent roots, all_gather of visits)" if world > 1 else "dp1"},
+                   "parallelism": f"dp{world} (independent roots, all_gather of visits/action/root Q)" if world > 1 else "dp1"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                     "traffic_source": {"key": tkey, "note": tnote,
+                                        "kernel_avg_ns_profiled": tent.get("avg_ns") if tent else None},
                      "kernel": kname, "kernel_ms": kern_ms,
                      "flop_per_launch": flops_launch, "sel_steps_per_sim": sel_sum / (B * S),
                      "measured_ceiling": {"value": FP32_MFMA_MEASURED_TFLOPS[wps],
@@ -406,6 +470,7 @@ def main():
                                                   "informational -- frac above is against the spec peak"},
                      "tree": tree},
         "cpu_baseline": cpu,
+        "build_id": _lib.build_id(),
     }
     if rank == 0:
         print(json.dumps(result), flush=True)

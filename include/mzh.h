@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MZH_ABI_VERSION 1
+#define MZH_ABI_VERSION 2
 
 #define MZH_OK 0
 #define MZH_ERR_ARG (-1)         /* bad argument / shape (ValueError in Python)              */
@@ -45,12 +45,18 @@ extern "C" {
 #define MZH_FLAG_KERNEL_COOP 2u /* force the cooperative kernel (4 waves share one 32-root tile) */
 #define MZH_FLAG_KERNEL_WAVE 4u /* force the wave-independent kernel, 32 roots per wave (default for B >= 53248) */
 #define MZH_FLAG_KERNEL_WAVE16 8u /* force the wave-independent kernel, 16 roots per wave (default for 8192 < B < 53248) */
+#define MZH_FLAG_COOP_TILE16 16u /* cooperative kernel: 16 roots per workgroup (default for B <= 4096) */
+#define MZH_FLAG_COOP_TILE32 32u /* cooperative kernel: 32 roots per workgroup (default for B > 4096) */
 
 typedef struct mzh_engine mzh_engine;
 typedef void* mzh_stream; /* hipStream_t */
 
 int mzh_abi_version(void);
 const char* mzh_last_error(void);
+/* Provenance: a hash of the csrc/ sources, include/mzh.h and the compiler flags this library was
+ * built from (muzero-hanoi_amd/build.py source_hash); the Python binding refuses a library whose id
+ * differs from the checked-out sources, and bench / smoke records print it. */
+const char* mzh_build_id(void);
 int mzh_device_count(int* count);
 
 /* ---------------------------------------------------------------------------------------------
@@ -154,6 +160,11 @@ typedef struct mzh_search_args {
   int32_t* latent;      /* [B][n_sims+1] moves of the last simulation's path (mcts.py:79-86) */
   int32_t* latent_len;  /* [B] */
   int32_t* sel_steps;   /* [B] total selection steps (sum of depths), for byte accounting */
+  /* play-policy power table (nullable): pow_table[n] = np.power(n, max(1, min(5, 1/T))) for
+   * n = 0..n_sims as the caller's NumPy computes it (mcts.py:168-174).  Read only for a non-integer
+   * exponent (integer exponents are exact products); without it the device pow is used, which can
+   * differ from NumPy's vectorised pow in the last bit. */
+  const double* pow_table;
 } mzh_search_args;
 
 int mzh_search(mzh_engine* eng, const mzh_search_args* args, mzh_stream stream);

@@ -11,8 +11,10 @@ import os
 import torch  # noqa: F401  (must precede loading libmzh.so, see above)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("MZH_LIB") or os.path.join(HERE, "libmzh.so")  # MZH_LIB: diagnostic builds
+DEFAULT_LIB = os.path.join(HERE, "libmzh.so")
+LIB_PATH = os.environ.get("MZH_LIB") or DEFAULT_LIB  # MZH_LIB: diagnostic builds
 
+ABI_VERSION = 2
 MZH_OK = 0
 MZH_ERR_ARG = -1
 MZH_ERR_HIP = -2
@@ -23,6 +25,8 @@ MZH_FLAG_NP1_UCB = 1
 MZH_FLAG_KERNEL_COOP = 2  # cooperative kernel (mzh_search.hip)
 MZH_FLAG_KERNEL_WAVE = 4  # wave-independent kernel (mzh_wave.hip), 32 roots per wave
 MZH_FLAG_KERNEL_WAVE16 = 8  # wave-independent kernel, 16 roots per wave
+MZH_FLAG_COOP_TILE16 = 16  # cooperative kernel, 16 roots per workgroup
+MZH_FLAG_COOP_TILE32 = 32  # cooperative kernel, 32 roots per workgroup
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -36,7 +40,7 @@ class SearchArgs(ctypes.Structure):
         ("obs", _vp), ("noise", _vp), ("tie_idx", _vp), ("action_u", _vp), ("minmax_in", _vp),
         ("rp_root_pi", _vp), ("rp_pi", _vp), ("rp_reward", _vp), ("rp_value", _vp),
         ("visits", _vp), ("root_q", _vp), ("minmax_out", _vp), ("extra_ties", _vp), ("action", _vp),
-        ("pi", _vp), ("latent", _vp), ("latent_len", _vp), ("sel_steps", _vp),
+        ("pi", _vp), ("latent", _vp), ("latent_len", _vp), ("sel_steps", _vp), ("pow_table", _vp),
     ]
 
 
@@ -55,6 +59,7 @@ class TrainArgs(ctypes.Structure):
 # name -> (restype, argtypes); every symbol include/mzh.h declares
 SIGNATURES = {
     "mzh_abi_version": (ctypes.c_int, []),
+    "mzh_build_id": (ctypes.c_char_p, []),
     "mzh_last_error": (ctypes.c_char_p, []),
     "mzh_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "mzh_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -90,10 +95,23 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.mzh_abi_version() != 1:
-            raise RuntimeError("libmzh.so ABI version mismatch")
+        if L.mzh_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"libmzh.so ABI version {L.mzh_abi_version()} != {ABI_VERSION}")
+        if os.path.abspath(LIB_PATH) == DEFAULT_LIB and os.path.isdir(os.path.join(HERE, "csrc")):
+            # provenance: the shipped library must be built from the checked-out sources
+            from . import build as _build
+
+            want, got = _build.source_hash(), L.mzh_build_id().decode()
+            if got != want:
+                raise RuntimeError(f"{LIB_PATH} was built from other sources or flags (build id {got}, the "
+                                   f"checked-out sources hash to {want}): rebuild with "
+                                   "`python -m muzero_hanoi_amd.build`")
         _lib = L
     return _lib
+
+
+def build_id():
+    return lib().mzh_build_id().decode()
 
 
 def last_error():

@@ -6,6 +6,7 @@
 tree arithmetic or the fp32 epilogues; see csrc/mzh_device.h).
 """
 import concurrent.futures as cf
+import hashlib
 import os
 import subprocess
 import sys
@@ -20,6 +21,39 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MZH_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off",
          "-Wall", "-Wno-unused-result", "-I", os.path.join(REPO, "include")]
+
+
+BUILD_ID_MARKER = b"MZH_BUILD_ID:"
+
+
+def source_files():
+    """every file the library is compiled from: csrc/*.hip, csrc/*.h and include/mzh.h"""
+    fs = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".h")))
+    return [os.path.join(CSRC, f) for f in fs] + [os.path.join(REPO, "include", "mzh.h")]
+
+
+def source_hash(flags=None):
+    """build id: sha256 over the sources' names and bytes and the compiler flags (first 20 hex)"""
+    h = hashlib.sha256()
+    for f in source_files():
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    # flags without the checkout's absolute path (the GPU box runs the same tree from another path)
+    h.update(" ".join(FLAGS if flags is None else flags).replace(REPO, "<repo>").encode())
+    return h.hexdigest()[:20]
+
+
+def embedded_build_id(lib_path):
+    """the build id compiled into a built library (read from the file, without loading it)"""
+    try:
+        with open(lib_path, "rb") as fh:
+            data = fh.read()
+    except OSError:
+        return None
+    i = data.find(BUILD_ID_MARKER)
+    return None if i < 0 else data[i + len(BUILD_ID_MARKER): i + len(BUILD_ID_MARKER) + 20].decode("ascii", "replace")
 
 
 def _stale(target, deps):
@@ -43,6 +77,9 @@ def build(verbose=False, force=False, diag=False, tag="", defines=()):
     want = " ".join(flags)
     if not os.path.exists(stamp) or open(stamp).read() != want:
         force = True
+    bid = source_hash(flags)
+    if embedded_build_id(lib_path) != bid:
+        force = True  # sources or flags differ from what the library was built from (not only mtimes)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     headers.append(os.path.join(REPO, "include", "mzh.h"))
     jobs = []
@@ -66,7 +103,14 @@ def build(verbose=False, force=False, diag=False, tag="", defines=()):
                 print(err, file=sys.stderr)
     objs = [os.path.join(obj_dir, s.replace(".hip", ".o")) for s in SOURCES]
     if force or jobs or _stale(lib_path, objs):
-        run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", lib_path,
+        # provenance: the build id as a host-only object linked into the library (mzh_build_id())
+        id_src = os.path.join(obj_dir, "mzh_build_id.cpp")
+        with open(id_src, "w") as f:
+            f.write(f'static const char kId[] = "{BUILD_ID_MARKER.decode()}{bid}";\n'
+                    'extern "C" const char* mzh_build_id(void) { return kId + %d; }\n' % len(BUILD_ID_MARKER))
+        id_obj = os.path.join(obj_dir, "mzh_build_id.o")
+        run(["g++", "-O2", "-fPIC", "-c", id_src, "-o", id_obj])
+        run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, id_obj, "-o", lib_path,
              "-Wl,-rpath,/opt/rocm/lib"])
     with open(stamp, "w") as f:
         f.write(want)

@@ -377,14 +377,11 @@ extern "C" int mzh_hanoi_solver(int n_disks, int goal_peg, int B, const uint8_t*
 static int pick_rows(int B) { return B > 256 * 16 ? 32 : 16; }
 
 // cooperative search tile: 16 roots while that is one round of workgroups (B <= 4,096), else 32
-// roots (a second round of 16-root workgroups costs more than 32-root tiles).  MZH_ROWS=16|32 in the
-// environment forces one (A/B experiments only).
-static int pick_tile(int B) {
-  static const int forced = [] {
-    const char* v = getenv("MZH_ROWS");
-    return v ? atoi(v) : 0;
-  }();
-  if (forced == 16 || forced == 32) return forced;
+// roots (a second round of 16-root workgroups costs more than 32-root tiles).  MZH_FLAG_COOP_TILE16 /
+// MZH_FLAG_COOP_TILE32 force one (tests reach both tiles' code paths at any batch size).
+static int pick_tile(int B, uint32_t flags) {
+  if (flags & MZH_FLAG_COOP_TILE16) return 16;
+  if (flags & MZH_FLAG_COOP_TILE32) return 32;
   return B > 256 * 16 ? 32 : 16;
 }
 
@@ -467,7 +464,7 @@ static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream s
     return fail(MZH_ERR_ARG, "stochastic action selection needs action_u");
   const KernelChoice kc = choose_kernel(a->B, a->flags);
   const bool wave = kc.wave;
-  int R = pick_tile(a->B);
+  int R = pick_tile(a->B, a->flags);
   if (wave) {
     if (mzh_wave_smem_bytes(a->n_sims, kc.nt) > kMaxLds)
       return fail(MZH_ERR_CAPACITY, "n_sims=%d exceeds the wave kernel's LDS table budget", a->n_sims);
@@ -487,6 +484,7 @@ static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream s
   p.tree = eng->tree; p.htree = eng->htree; p.pathx = eng->pathx; p.table = eng->table;
   p.visits = a->visits; p.root_q = a->root_q; p.minmax_out = a->minmax_out; p.extra_ties = a->extra_ties;
   p.action = a->action; p.pi = a->pi; p.latent = a->latent; p.latent_len = a->latent_len; p.sel_steps = a->sel_steps;
+  p.pow_table = a->pow_table;
   hipError_t e = wave ? mzh_launch_wave_search(kc.nt, replay, eng->wnet, p, (hipStream_t)stream)
                       : mzh_launch_search(R, replay, eng->net, p, (hipStream_t)stream);
   return e == hipSuccess ? MZH_OK : hip_fail(e, "search launch");

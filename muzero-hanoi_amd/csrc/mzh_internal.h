@@ -33,7 +33,22 @@ struct MzhSearchParams {
   int32_t* latent;
   int32_t* latent_len;
   int32_t* sel_steps;
+  const double* pow_table;  // [S + 1] np.power(n, 1/T) for a non-integer exponent (nullable)
 };
+
+// visits ** e as generate_play_policy computes it (np.power(int64 visits, e), mcts.py:168-174), for
+// x = n visits and e = max(1, min(5, 1/T)): an integer exponent is an exact product (n^5 < 2^53);
+// a non-integer one is taken from pow_table[n], the caller's np.power(arange(S + 1), e) (NumPy's
+// vectorised pow -- SVML on AVX-512 hosts -- differs from any other pow in the last bit for some
+// n), or from the device pow when no table is given
+__device__ __forceinline__ double mzh_pow(double x, int n, double e, const double* pow_table) {
+  if (e == __builtin_rint(e)) {
+    double r = x;
+    for (int i = 1; i < (int)e; ++i) r = r * x;
+    return r;
+  }
+  return pow_table ? pow_table[n] : pow(x, e);
+}
 
 struct MzhInferParams {
   int B, in_dim, kin;

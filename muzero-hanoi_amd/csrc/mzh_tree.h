@@ -123,15 +123,6 @@ __device__ __forceinline__ int mzh_group_pick(float ucb, int c, int lane, int ti
   return six ? tie : first;
 }
 
-// x ** e with numpy semantics for the exponents generate_play_policy can produce
-__device__ __forceinline__ double mzh_pow(double x, double e) {
-  if (e == __builtin_rint(e) && e >= 1.0 && e <= 5.0) {
-    double r = x;
-    for (int i = 1; i < (int)e; ++i) r = r * x;
-    return r;
-  }
-  return pow(x, e);
-}
 
 
 // A root's search state between the tree steps, held in registers by every lane of its 8-lane group
@@ -446,7 +437,7 @@ struct MzhTree {
         double ex = 1.0 / p.temperature;
         ex = ex < 5.0 ? ex : 5.0;  // max(1.0, min(5.0, 1/T))
         ex = ex > 1.0 ? ex : 1.0;
-        for (int a = 0; a < MZH_A; ++a) v[a] = mzh_pow(v[a], ex);
+        for (int a = 0; a < MZH_A; ++a) v[a] = mzh_pow(v[a], vis[a], ex, p.pow_table);
       }
       double sum = 0.0;
       for (int a = 0; a < MZH_A; ++a) sum = sum + v[a];

@@ -527,7 +527,10 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
           const uint3 hnx = *reinterpret_cast<const uint3*>(blk + 12 * half);
           const uint3 hR = *reinterpret_cast<const uint3*>(blk + 24 + 12 * half);
           const uint3 hP = *reinterpret_cast<const uint3*>(blk + 48 + 12 * half);
-          const uint4 hW01 = *reinterpret_cast<const uint4*>(blk + 72 + 24 * half);
+          // the W pair at byte 72 + 24 half is only 8-byte aligned: an 8-byte-aligned 16-byte type, so
+          // no 16-byte alignment is implied (still one dwordx4: gfx950 global loads need 4-byte alignment)
+          typedef unsigned int u32x4_a8 __attribute__((ext_vector_type(4), aligned(8)));
+          const u32x4_a8 hW01 = *reinterpret_cast<const u32x4_a8*>(blk + 72 + 24 * half);
           const uint2 hW2 = *reinterpret_cast<const uint2*>(blk + 88 + 24 * half);
           const int hn[3] = {(int)hnx.x, (int)hnx.y, (int)hnx.z};
           const float hr[3] = {__uint_as_float(hR.x), __uint_as_float(hR.y), __uint_as_float(hR.z)};
@@ -851,15 +854,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
       double ex = 1.0 / p.temperature;
       ex = ex < 5.0 ? ex : 5.0;  // max(1.0, min(5.0, 1/T))
       ex = ex > 1.0 ? ex : 1.0;
-      for (int a = 0; a < MZH_A; ++a) {
-        if (ex == __builtin_rint(ex)) {
-          double r = v[a];
-          for (int i = 1; i < (int)ex; ++i) r = r * v[a];
-          v[a] = r;
-        } else {
-          v[a] = pow(v[a], ex);
-        }
-      }
+      for (int a = 0; a < MZH_A; ++a) v[a] = mzh_pow(v[a], vis[a], ex, p.pow_table);
     }
     double sum = 0.0;
     for (int a = 0; a < MZH_A; ++a) sum = sum + v[a];

@@ -3,8 +3,10 @@
 Roots are independent, so the search shards with no data-path collective: rank r owns the
 contiguous slice [r*B/W, (r+1)*B/W) of the global batch.  Every random draw is made for the
 GLOBAL batch in global root order and then sliced, so results do not depend on the world size.
-The single exchange is an all_gather of the int32 visit histograms (RCCL over xGMI on the GPUs,
-gloo in the CPU tests); weights are broadcast once at start-up.
+The single exchange is one all_gather of each root's search result -- what run_mcts returns
+(MCTS/mcts.py:122-126): the visit histogram, the action and root Q (fp64) -- packed as 9 int32
+words per root (RCCL over xGMI on the GPUs, gloo in the CPU tests); weights are broadcast once
+at start-up.
 """
 import numpy as np
 import torch
@@ -32,9 +34,9 @@ def broadcast_weights(flat, device, src=0):
     return t.cpu().numpy()
 
 
-def gather_visits(local, B, world):
-    """all_gather of per-rank [b_r, 6] int32 visit histograms -> global [B, 6] in root order.
-    Shards may differ by one root: each rank pads to the largest shard size."""
+def gather_rows(local, B, world):
+    """all_gather of per-rank [b_r, k] rows -> global [B, k] in root order.  Shards may differ by
+    one root: each rank pads to the largest shard size."""
     bmax = shard_range(B, world, 0)[1]  # rank 0 holds the largest shard
     pad = torch.zeros((bmax, local.shape[1]), dtype=local.dtype, device=local.device)
     pad[: local.shape[0]] = local
@@ -45,3 +47,27 @@ def gather_visits(local, B, world):
         s, e = shard_range(B, world, r)
         parts.append(out[r * bmax: r * bmax + (e - s)])
     return torch.cat(parts)
+
+
+def gather_visits(local, B, world):
+    """all_gather of per-rank [b_r, 6] int32 visit histograms -> global [B, 6] in root order"""
+    return gather_rows(local, B, world)
+
+
+def pack_results(visits, action, root_q):
+    """[b, 9] int32: visits (6), action (1), root Q's fp64 bits (2) -- one collective per search"""
+    b = visits.shape[0]
+    return torch.cat([visits.to(torch.int32).reshape(b, 6), action.to(torch.int32).reshape(b, 1),
+                      root_q.to(torch.float64).contiguous().view(torch.int32).reshape(b, 2)], 1)
+
+
+def unpack_results(packed):
+    b = packed.shape[0]
+    return dict(visits=packed[:, :6].contiguous(), action=packed[:, 6].contiguous(),
+                root_q=packed[:, 7:9].contiguous().view(torch.float64).reshape(b))
+
+
+def gather_results(out, B, world):
+    """the global batch's visits [B, 6] int32, action [B] int32 and root_q [B] fp64 in root order,
+    from every rank's search outputs (one all_gather of the packed rows)"""
+    return unpack_results(gather_rows(pack_results(out["visits"], out["action"], out["root_q"]), B, world))

@@ -123,12 +123,29 @@ class Engine:
             sel_steps=torch.empty(B, dtype=torch.int32, device=d),
         )
 
+    def pow_table(self, n_sims, temperature):
+        """play-policy power table for a non-integer exponent (None otherwise): np.power over
+        arange(n_sims + 1) as int64 with the Python-float exponent, exactly the call
+        generate_play_policy makes on the visit counts (MCTS/mcts.py:168-174), on the device"""
+        if not 0.0 < temperature <= 1.0:
+            return None
+        e = max(1.0, min(5.0, 1.0 / temperature))
+        if e == int(e):
+            return None
+        cache = self.__dict__.setdefault("_pow_tables", {})
+        key = (int(n_sims), float(temperature))
+        if key not in cache:
+            tab = np.power(np.arange(n_sims + 1, dtype=np.int64), e)
+            cache[key] = torch.from_numpy(tab).to(self.device)
+        return cache[key]
+
     def search(self, n_sims, *, obs=None, replay=None, tie_idx, noise=None, action_u=None, minmax_in=None,
                temperature=1.0, deterministic=False, discount=0.8, eps=0.25, np1_ucb=False, out=None,
-               kernel=None):
+               kernel=None, tile=None):
         """Batched search. Tensors must already be on the device (bench: inputs resident in HBM).
         replay = dict(root_pi, pi, reward, value) -> tree-only mode (mzh_search_replay).
-        kernel = None (automatic by batch size) | "coop" | "wave" | "wave16" (all give identical results)."""
+        kernel = None (automatic by batch size) | "coop" | "wave" | "wave16" (all give identical results);
+        tile = None | 16 | 32: the cooperative kernel's roots per workgroup (default by batch size)."""
         B = int(tie_idx.shape[0])
         if out is None:
             out = self.alloc_search_outputs(B, n_sims)
@@ -151,6 +168,7 @@ class Engine:
         a.flags = (_lib.MZH_FLAG_NP1_UCB if np1_ucb else 0) | {None: 0, "coop": _lib.MZH_FLAG_KERNEL_COOP,
                                                                "wave": _lib.MZH_FLAG_KERNEL_WAVE,
                                                                "wave16": _lib.MZH_FLAG_KERNEL_WAVE16}[kernel]
+        a.flags |= {None: 0, 16: _lib.MZH_FLAG_COOP_TILE16, 32: _lib.MZH_FLAG_COOP_TILE32}[tile]
         a.obs = ptr(dev(obs, torch.float32))
         a.noise = ptr(dev(noise, torch.float64))
         a.tie_idx = ptr(dev(tie_idx, torch.int32))
@@ -170,6 +188,11 @@ class Engine:
         a.latent = ptr(out.get("latent"))
         a.latent_len = ptr(out.get("latent_len"))
         a.sel_steps = ptr(out.get("sel_steps"))
+        pt = self.pow_table(n_sims, float(temperature)) if (out.get("pi") is not None or
+                                                              out.get("action") is not None) else None
+        if pt is not None:
+            keep.append(pt)
+        a.pow_table = ptr(pt)
         fn = _lib.lib().mzh_search_replay if replay is not None else _lib.lib().mzh_search
         check(fn(self._h, ctypes.byref(a), self._stream()), "mzh_search")
         out["_keep"] = keep  # inputs stay alive until the caller is done with the async call

@@ -89,10 +89,17 @@ class MCTS:
         if self.pb_c_base != 19652 or self.pb_c_init != 1.25:
             raise NotImplementedError("libmzh bakes pb_c_base=19652, pb_c_init=1.25 (mcts.py:24-25)")
         S = int(self.n_simulations)
+        # the reference raises for a bad temperature inside generate_play_policy (mcts.py:113,
+        # 163-166): after the whole search (Dirichlet draw, argmax tie draws, MinMaxStats updates,
+        # latent_actions) and before the action draw (mcts.py:120).  So the search runs, its state
+        # is kept, no action uniform is drawn, then the ValueError.
+        bad_t = not 0.0 <= temperature <= 1.0
         noise, tie, u = _rng.predraw(1, deterministic=deterministic, alpha=self.root_dirichlet_alpha,
-                                     eps=self.root_exploration_eps)
-        if not 0.0 <= temperature <= 1.0:  # raised after the search's draws, like mcts.py:163-166
-            raise ValueError(f"Expect `temperature` to be in the range [0.0, 1.0], got {temperature}")
+                                     eps=self.root_exploration_eps, draw_action=not bad_t)
+        if bad_t:
+            deterministic, temperature_k = True, 0.0  # the kernel's policy output is discarded
+        else:
+            temperature_k = temperature
         replay = None
         if isinstance(network, RecordedNetwork):
             eng = _replay_engine(network.n_disks, S)
@@ -117,7 +124,7 @@ class MCTS:
         d = pin.d
         out = eng.search(S, obs=None if replay else d["obs"], replay=replay, tie_idx=d["tie"],
                          noise=None if noise is None else d["noise"], action_u=None if u is None else d["u"],
-                         minmax_in=d["mm"], temperature=float(temperature), deterministic=bool(deterministic),
+                         minmax_in=d["mm"], temperature=float(temperature_k), deterministic=bool(deterministic),
                          discount=float(self.discount), eps=float(self.root_exploration_eps), np1_ucb=self.np1_ucb,
                          out=dict(pout.d))
         pout.to_host()
@@ -130,6 +137,8 @@ class MCTS:
         if self.last_extra_ties:
             warnings.warn("search met an argmax tie beyond the root's first selection: the NumPy RNG stream "
                           "now differs from the reference's", RuntimeWarning)
+        if bad_t:
+            raise ValueError(f"Expect `temperature` to be in the range [0.0, 1.0], got {temperature}")
         return int(host["action"][0]), host["pi"][0].astype(np.float64), float(host["root_q"][0])
 
     def return_latent_actions(self):

@@ -7,7 +7,10 @@ Same constructor and `training_loop(n_loops, min_replay_size, print_acc)` as the
     n_ep_x_loop episodes of a loop play in lockstep -- one search launch and one env-kernel launch
     per step for all of them (selfplay.BatchedSelfPlay), each episode an agent whose MinMaxStats
     starts from the MCTS instance's, then the reference's per-episode bookkeeping
-    (selfplay.episode_records) and buffer filter;
+    (selfplay.episode_records) and buffer filter.  With n_ep_x_loop > 1 that is NOT the
+    reference's schedule (one MinMaxStats chain through the episodes in order, Muzero.py:55; other
+    per-step draw interleaving): a RuntimeWarning says so, and "sequential" (the default) is the
+    parity mode;
   * the replay buffer keeps its transitions on the training device (buffer.Buffer);
   * the update (`_update`, Muzero.py:209-274): the 5-step unrolled loss of the reference -- the
     same torch operations in the same order (represent, prediction/dynamics per unroll step,
@@ -18,6 +21,7 @@ Same constructor and `training_loop(n_loops, min_replay_size, print_acc)` as the
 import ctypes
 import logging
 import math
+import warnings
 
 import numpy as np
 import torch
@@ -63,6 +67,13 @@ class Muzero:
         # Muzero._play_game runs them; "batched" = a loop's n_ep_x_loop episodes in lockstep
         if selfplay not in ("sequential", "batched"):
             raise ValueError(f"selfplay must be 'sequential' or 'batched', not {selfplay!r}")
+        if selfplay == "batched" and n_ep_x_loop > 1:
+            # not the reference's algorithm: the reference threads ONE MinMaxStats through its
+            # episodes in order (Muzero.py:55) and interleaves the per-step draws differently
+            warnings.warn("Muzero(selfplay='batched') with n_ep_x_loop > 1 plays the loop's episodes in lockstep, "
+                          "each from the same MinMaxStats (the union kept afterwards) with its own draw order: "
+                          "not the reference's sequential schedule; use selfplay='sequential' for parity runs",
+                          RuntimeWarning, stacklevel=2)
         self.selfplay = selfplay
 
     # ------------------------------------------------------------------ Muzero.py:81-151

@@ -23,13 +23,14 @@ def uses_noise(deterministic, alpha, eps):
     return (not deterministic) and alpha > 0.0 and eps > 0.0
 
 
-def predraw(n_roots, *, deterministic, alpha, eps=0.25, rng=None):
+def predraw(n_roots, *, deterministic, alpha, eps=0.25, rng=None, draw_action=True):
     """Draw (noise[B,6] f64 | None, tie[B] i32, u[B] f64 | None) from `rng` (default: the
-    global legacy NumPy stream, exactly as the reference consumes it)."""
+    global legacy NumPy stream, exactly as the reference consumes it).  draw_action=False: a
+    search that raises before its action draw (invalid temperature, mcts.py:113,163-166)."""
     rs = np.random if rng is None else rng
     noise = np.empty((n_roots, 6), np.float64) if uses_noise(deterministic, alpha, eps) else None
     tie = np.empty(n_roots, np.int32)
-    u = None if deterministic else np.empty(n_roots, np.float64)
+    u = None if (deterministic or not draw_action) else np.empty(n_roots, np.float64)
     alphas = np.ones(6, np.float32) * alpha  # np.ones_like(prob) * alpha with prob float32
     cand = np.arange(6)
     for r in range(n_roots):

@@ -242,7 +242,11 @@ def evaluate(network, n_disks, n_sims_range, *, episodes=1, start=None, start_id
     included) from the global NumPy stream -- get_results' schedule.  Otherwise each budget's
     episodes run as one batch, each episode its own agent with a fresh MinMaxStats.
     Returns dict(data=[[n, mean error]] (get_results' value), illegal=[[n, mean rate, std error]]
-    (illegal_move_rate's value per budget), errors / steps / illegal_rates per budget, minmax)."""
+    (illegal_move_rate's value per budget), errors / steps / illegal_rates per budget, minmax).
+    minmax (in and out) is the carried chain of the sequential schedule only: with
+    sequential=False every agent starts fresh, `minmax` must be None and None is returned."""
+    if not sequential and minmax is not None:
+        raise ValueError("evaluate: minmax applies to the sequential schedule only (batched agents start fresh)")
     legacy_rng = sequential if legacy_rng is None else legacy_rng
     data, illegal, errors_all, steps_all, rates_all = [], [], [], [], []
     mm = None if minmax is None else np.asarray(minmax, np.float64).reshape(1, 2)
@@ -289,4 +293,4 @@ def evaluate(network, n_disks, n_sims_range, *, episodes=1, start=None, start_id
         steps_all.append(steps)
         rates_all.append(rates)
     return dict(data=data, illegal=illegal, errors=errors_all, steps=steps_all, illegal_rates=rates_all,
-                minmax=mm)
+                minmax=mm if sequential else None)

@@ -551,8 +551,12 @@ static void search_one(int S, double discount, int flags, const orc_net* net, co
 
 /* generate_play_policy + action choice (mcts.py:111-122, 154-176) and legacy
  * RandomState.choice(6, p=pi): cdf = cumsum(p); cdf /= cdf[-1]; searchsorted(u, 'right').
+ * powtab (nullable): powtab[n] = np.power(n, e) as the caller's NumPy computes it (mcts.py:174);
+ * used for a non-integer exponent, where NumPy's vectorised pow (SVML on AVX-512 hosts) and libm's
+ * pow differ in the last bit for some n.  Integer exponents are exact products either way.
  * Returns -1 on an invalid temperature (ValueError). */
-int orc_play_policy(const int* visits, double temperature, int deterministic, double u, double* pi) {
+int orc_play_policy(const int* visits, double temperature, int deterministic, double u, const double* powtab,
+                    double* pi) {
   if (!(temperature >= 0.0 && temperature <= 1.0)) return -1;
   double v[ORC_A];
   for (int a = 0; a < ORC_A; ++a) v[a] = (double)visits[a];
@@ -560,7 +564,8 @@ int orc_play_policy(const int* visits, double temperature, int deterministic, do
     double e = 1.0 / temperature;
     if (e > 5.0) e = 5.0;
     if (e < 1.0) e = 1.0;
-    for (int a = 0; a < ORC_A; ++a) v[a] = pow(v[a], e);
+    const int integral = e == rint(e);
+    for (int a = 0; a < ORC_A; ++a) v[a] = (powtab && !integral) ? powtab[visits[a]] : pow(v[a], e);
   }
   double sum = 0.0;
   for (int a = 0; a < ORC_A; ++a) sum += v[a];
@@ -591,7 +596,7 @@ int orc_search(int n_disks, int S, int B, double discount, int flags, const floa
                int support, const float* obs, const float* rp_root_pi, const float* rp_pi,
                const float* rp_rwd, const float* rp_val, const double* noise, double eps,
                const int* tie_idx, const double* action_u, double temperature, int deterministic,
-               const double* minmax_in, int* visits, double* rootQ, double* minmax_out,
+               const double* powtab, const double* minmax_in, int* visits, double* rootQ, double* minmax_out,
                int* extra_ties, int* action, double* pi, int* latent, int* latent_len,
                long* sel_steps) {
   int in_dim = 3 * n_disks;
@@ -630,7 +635,7 @@ int orc_search(int n_disks, int S, int B, double discount, int flags, const floa
     if (action || pi) {
       double p[ORC_A];
       int act = orc_play_policy(visits + (size_t)b * ORC_A, temperature, deterministic,
-                                action_u ? action_u[b] : 0.0, p);
+                                action_u ? action_u[b] : 0.0, powtab, p);
       if (act < 0) status = -2;
       if (action) action[b] = act;
       if (pi) memcpy(pi + (size_t)b * ORC_A, p, sizeof(p));

@@ -62,13 +62,14 @@ def lib():
         L.orc_recurrent_inference.restype = None
         L.orc_recurrent_inference.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 9
         L.orc_play_policy.restype = ctypes.c_int
-        L.orc_play_policy.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_void_p]
+        L.orc_play_policy.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_void_p,
+                                      ctypes.c_void_p]
         L.orc_search.restype = ctypes.c_int
         L.orc_search.argtypes = (
             [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_void_p,
              ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p,
-             ctypes.c_double, ctypes.c_int, ctypes.c_void_p] + [ctypes.c_void_p] * 9)
+             ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_void_p] * 9)
     return _lib
 
 
@@ -155,10 +156,24 @@ def recurrent_inference(flat, in_dim, support, h_in, actions):
     return dict(h=h, reward=r, pi=pi, value=v, policy_logits=pl, value_logits=vl, reward_logits=rl)
 
 
+def numpy_pow_table(n_max, temperature):
+    """np.power(n, exp) for n = 0..n_max exactly as generate_play_policy computes it (MCTS/mcts.py:168-174:
+    an int64 array raised to a Python float), or None where no power is taken or the exponent is an
+    integer (exact products).  NumPy's float64 power is vectorised (SVML on AVX-512 hosts) and differs
+    from libm's pow in the last bit for some n, so the C restatement takes the values from NumPy."""
+    if not 0.0 < temperature <= 1.0:
+        return None
+    e = max(1.0, min(5.0, 1.0 / temperature))
+    if e == int(e):
+        return None
+    return np.power(np.arange(n_max + 1, dtype=np.int64), e)
+
+
 def play_policy(visits, temperature, deterministic, u=0.0):
     v = np.ascontiguousarray(visits, np.int32)
     pi = np.zeros(6, np.float64)
-    a = lib().orc_play_policy(_p(v), float(temperature), int(deterministic), float(u), _p(pi))
+    pt = _c(numpy_pow_table(int(v.max()) if v.size else 0, temperature), np.float64)
+    a = lib().orc_play_policy(_p(v), float(temperature), int(deterministic), float(u), _p(pt), _p(pi))
     return a, pi
 
 
@@ -188,9 +203,10 @@ def search(n_disks, S, obs, *, flat=None, support=33, replay=None, noise=None, e
     tie = _c(tie_idx if tie_idx is not None else np.zeros(B), np.int32)
     au = _c(action_u, np.float64)
     mmi = _c(minmax_in, np.float64)
+    pt = _c(numpy_pow_table(S, temperature), np.float64)
     st = lib().orc_search(n_disks, S, B, float(discount), 1 if np1_ucb else 0, _p(flat), support,
                           _p(obs), _p(rp[0]), _p(rp[1]), _p(rp[2]), _p(rp[3]), _p(noise), float(eps),
-                          _p(tie), _p(au), float(temperature), int(deterministic), _p(mmi),
+                          _p(tie), _p(au), float(temperature), int(deterministic), _p(pt), _p(mmi),
                           _p(visits), _p(rootQ), _p(mm), _p(et), _p(action), _p(pi), _p(latent),
                           _p(latent_len), _p(steps))
     if st == -2:

@@ -24,6 +24,10 @@ Fixtures (see tests/golden/README.md):
   ucb_np1_vs_np2.npz      child_U under NumPy-2 (the reference's own, here) and NumPy-1 promotion
   tie_replay.npz          a run_mcts trace with argmax ties beyond the root's first selection
   random_reset.npz        TowersOfHanoi.random_reset start states from a seeded global stream
+  play_policy.npz         generate_play_policy over random histograms at non-integer exponents
+  bad_temperature.npz     run_mcts with invalid temperatures between valid ones (state after the raise)
+  agree_<case>.npz        the reference's run_mcts (torch-CPU network) on 256-1024 roots per
+                          (N, S) shape: visit histograms + root-level UCB gaps (near-tie report)
 """
 import json
 import os
@@ -329,6 +333,139 @@ REPLAY_CASES = [
     ("n7s100_sto", 7, 100, 3, False, 0.25, 1.0, {}),
     ("n3s25_mc", 3, 25, 4, False, 0.25, 1.0, {"td": False}),
     ("n4s1_sto", 4, 1, 4, False, 0.25, 1.0, {}),
+    # non-integer play-policy exponents (np.power with 1/T = 3.33.., 1.43.., 1.11..; mcts.py:173-174)
+    ("n4s50_sto_t03", 4, 50, 6, False, 0.25, 0.3, {}),
+    ("n4s50_sto_t07", 4, 50, 6, False, 0.25, 0.7, {}),
+    ("n3s25_sto_t09", 3, 25, 8, False, 0.25, 0.9, {}),
+]
+
+
+def gen_play_policy(n_hist=600, seed=71):
+    """MCTS.generate_play_policy (mcts.py:154-176) of the reference over random visit histograms
+    (sums S in {1, 25, 50, 100, 200}, zeros included) at temperatures with non-integer exponents
+    (and a few integer ones): the NumPy np.power values the play policy is built from."""
+    m = MCTS(discount=0.8, root_dirichlet_alpha=0.25, n_simulations=1, batch_s=1, device="cpu")
+    rs = np.random.RandomState(seed)
+    temps = np.array([0.3, 0.7, 0.9, 0.35, 0.45, 0.6, 0.8, 0.95, 0.999, 0.21, 1.0, 0.5, 0.25], np.float64)
+    hist, sums = [], []
+    for i in range(n_hist):
+        S = [1, 25, 50, 100, 200][i % 5]
+        k = rs.randint(1, 7)  # children with visits
+        p = rs.dirichlet(np.full(k, 0.5))
+        v = np.zeros(6, np.int64)
+        v[rs.choice(6, k, replace=False)] = rs.multinomial(S, p)
+        hist.append(v)
+        sums.append(S)
+    hist = np.array(hist, np.int64)
+    pi = np.array([[m.generate_play_policy(h, float(t)) for h in hist] for t in temps], np.float64)
+    # the raw powers too, elementwise over 0..200 (the table a device pow must reproduce)
+    powers = np.array([np.power(np.arange(201, dtype=np.int64), max(1.0, min(5.0, 1.0 / float(t))))
+                       for t in temps], np.float64)
+    np.savez_compressed(os.path.join(HERE, "play_policy.npz"), temps=temps, visits=hist.astype(np.int32),
+                        sums=np.array(sums, np.int32), pi=pi, powers=powers)
+
+
+def gen_agreement(name, n, s, n_roots, seed, wseed=0, alpha=0.25, temperature=1.0, discount=0.8):
+    """End to end at scale (hard part 2): the reference's own run_mcts with its
+    torch-CPU MuZeroNet on n_roots random non-goal roots, the global NumPy stream re-seeded with
+    seed + r before root r (so every root's draws are reproducible on their own).  Per root the
+    visit histogram, and the gap between the largest and second-largest float32 UCB score
+    (node.py:83-88): its minimum over the root-level decisions and over the deeper ones of visited
+    nodes -- the near-tie diagnostic for roots whose histograms an ulp-level MLP difference could
+    flip."""
+    from MCTS.node import Node
+
+    net = make_net(n, wseed, True)
+    env = TowersOfHanoi(N=n, max_steps=200)
+    goal = state_index(env.goal, n)
+    rs = np.random.RandomState(seed + 17)
+    root_idx = []
+    while len(root_idx) < n_roots:
+        i = int(rs.randint(3 ** n))
+        if i != goal:
+            root_idx.append(i)
+    margins, deep = [], []
+    orig = Node.best_child
+
+    def best_child(self, config, min_max_stats):
+        u = self.child_Q(config, min_max_stats) + self.child_U(config)
+        srt = np.sort(u)
+        gap = float(srt[-1] - srt[-2])
+        if self.parent is None:  # a root-level decision
+            margins[-1].append(gap)
+        elif self.N > 0:  # a deeper decision (N = 0: the uniform-prior tie of a fresh node)
+            deep[-1] = min(deep[-1], gap)
+        return orig(self, config, min_max_stats)
+
+    Node.best_child = best_child
+    visits, obs_all, min_gap, n_zero = [], [], [], []
+    try:
+        for r, idx in enumerate(root_idx):
+            np.random.seed(seed + r)
+            margins.append([])
+            deep.append(np.inf)
+            mcts = TracingMCTS(discount=discount, root_dirichlet_alpha=alpha, n_simulations=s, batch_s=256,
+                               device="cpu")
+            obs = np.zeros(3 * n)
+            obs[np.arange(n) * 3 + np.array(env.states[idx])] = 1.0
+            with torch.no_grad():
+                mcts.run_mcts(obs, net, temperature, False)
+            visits.append(mcts.last_visits.astype(np.int32))
+            obs_all.append(obs)
+            gaps = np.array(margins[-1][1:])  # the first decision is the 6-way tie at N_root = 0
+            min_gap.append(float(gaps.min()) if gaps.size else np.inf)
+            n_zero.append(int((gaps == 0).sum()))
+    finally:
+        Node.best_child = orig
+    np.savez_compressed(os.path.join(HERE, f"agree_{name}.npz"), n=n, s=s, seed=seed, wseed=wseed, alpha=alpha,
+                        temperature=temperature, discount=discount, root_idx=np.array(root_idx, np.int32),
+                        obs=np.array(obs_all, np.float32), visits=np.array(visits, np.int32),
+                        min_root_gap=np.array(min_gap, np.float64), zero_gaps=np.array(n_zero, np.int32),
+                        min_deep_gap=np.array(deep, np.float64))
+
+
+def gen_bad_temperature(n=3, s=25, seed=81, wseed=0):
+    """run_mcts calls on one MCTS instance with an invalid temperature between valid ones: the
+    reference runs the whole search (Dirichlet and tie draws, MinMaxStats, latent_actions) and
+    raises in generate_play_policy (mcts.py:113,163-166) before its action draw (mcts.py:120)."""
+    net = make_net(n, wseed, True)
+    env = TowersOfHanoi(N=n, max_steps=200)
+    temps = [1.5, 1.0, -0.1, 0.5]
+    roots = [3, 11, 7, 20]
+    np.random.seed(seed)
+    mcts = TracingMCTS(discount=0.8, root_dirichlet_alpha=0.25, n_simulations=s, batch_s=256, device="cpu")
+    rec = dict(obs=[], raised=[], action=[], pi=[], mm_max=[], mm_min=[], latent=[], out_pi=[], out_rwd=[],
+               out_v=[])
+    for t, idx in zip(temps, roots):
+        obs = np.zeros(3 * n)
+        obs[np.arange(n) * 3 + np.array(env.states[idx])] = 1.0
+        recorder = Recorder(net)
+        raised, action, pi = 0, -1, np.full(6, np.nan)
+        try:
+            action, pi, _ = mcts.run_mcts(obs, recorder, t, False)
+        except ValueError:
+            raised = 1
+        rec["obs"].append(obs)
+        rec["raised"].append(raised)
+        rec["action"].append(int(action))
+        rec["pi"].append(np.asarray(pi, np.float64))
+        rec["mm_max"].append(float(mcts.min_max_stats.maximum))
+        rec["mm_min"].append(float(mcts.min_max_stats.minimum))
+        lat = [int(x.item()) for x in mcts.return_latent_actions()]
+        rec["latent"].append(lat + [-1] * (s + 2 - len(lat)))
+        rec["out_pi"].append(np.array([c[3][2] for c in recorder.calls], np.float32))
+        rec["out_rwd"].append(np.array([c[3][1] for c in recorder.calls], np.float64))
+        rec["out_v"].append(np.array([c[3][3] for c in recorder.calls], np.float64))
+    post = np.random.random_sample(4)
+    np.savez_compressed(os.path.join(HERE, "bad_temperature.npz"), n=n, s=s, seed=seed, temps=np.array(temps),
+                        post_rng=post, **{k: np.array(v) for k, v in rec.items()})
+
+
+AGREE_CASES = [
+    # name, n, s, roots, seed: BASELINE configs[1..3]'s shape (4,50), configs[3]'s (4,200), configs[4]'s (7,100)
+    ("n4s50", 4, 50, 1024, 100_000),
+    ("n4s200", 4, 200, 256, 200_000),
+    ("n7s100", 7, 100, 256, 300_000),
 ]
 
 
@@ -694,6 +831,17 @@ EPISODE_CASES = [
 
 
 def main():
+    if "--policy-only" in sys.argv:
+        gen_play_policy()
+        gen_bad_temperature()
+        for name, n, s_, roots, det, alpha, t, extra in REPLAY_CASES:
+            if "_t0" in name[-4:] or name.endswith(("_t03", "_t07", "_t09")):
+                gen_replay(name, n, s_, roots, det, alpha, t, **extra)
+        return
+    if "--agree-only" in sys.argv:
+        for c in AGREE_CASES:
+            gen_agreement(*c)
+        return
     if "--corners-only" in sys.argv:
         print("ucb rows differing", gen_ucb_rules())
         print("tie counts", gen_tie_replay())
@@ -708,6 +856,10 @@ def main():
     gen_ucb_rules()
     gen_tie_replay()
     gen_random_reset()
+    gen_play_policy()
+    gen_bad_temperature()
+    for c in AGREE_CASES:
+        gen_agreement(*c)
     for c in ACTING_CASES:
         gen_acting(*c)
     for c in ILLEGAL_CASES:

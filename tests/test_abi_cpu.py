@@ -35,38 +35,64 @@ def test_library_exports_every_declared_symbol(lib):
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(lib.SIGNATURES), "ctypes signature table out of sync with include/mzh.h"
-    assert L.mzh_abi_version() == 1
+    assert L.mzh_abi_version() == lib.ABI_VERSION == 2
 
 
-def test_search_args_layout_matches_header(lib):
-    # the C struct: 2 x int32, 3 x double, int32, uint32, 18 pointers
-    assert ctypes.sizeof(lib.SearchArgs) == 8 + 24 + 8 + 18 * 8
-    assert lib.SearchArgs.obs.offset == 40
-    hdr = open(HEADER).read()
-    block = hdr[hdr.index("typedef struct mzh_search_args"):]
-    block = block[:block.index("} mzh_search_args;")]
-    n_ptr_fields = len(re.findall(r"^\s+(?:const\s+)?\w+\*\s+\w+;", block, re.M))
-    assert n_ptr_fields == 18
-
-
-def test_train_args_layout_matches_header(lib, tmp_path):
-    """ctypes TrainArgs == struct mzh_train_args as the C compiler lays it out"""
+def _c_offsets(struct, fields, tmp_path):
+    """offsetof of each field and sizeof of `struct` as the C compiler lays out include/mzh.h"""
     import shutil
     import subprocess
 
     cc = shutil.which("gcc") or shutil.which("cc")
     if cc is None:
         pytest.skip("no C compiler")
-    fields = [f[0] for f in lib.TrainArgs._fields_]
-    src = tmp_path / "off.c"
+    src = tmp_path / f"{struct}.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "mzh.h"\nint main(void){\n'
-                   + "".join(f'printf("%zu\\n", offsetof(mzh_train_args, {f}));\n' for f in fields)
-                   + 'printf("%zu\\n", sizeof(mzh_train_args)); return 0; }\n')
-    exe = tmp_path / "off"
+                   + "".join(f'printf("%zu\\n", offsetof({struct}, {f}));\n' for f in fields)
+                   + f'printf("%zu\\n", sizeof({struct})); return 0; }}\n')
+    exe = tmp_path / struct
     subprocess.run([cc, "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)], check=True)
-    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    return [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+
+
+def test_search_args_layout_matches_header(lib, tmp_path):
+    """ctypes SearchArgs == struct mzh_search_args as the C compiler lays it out"""
+    fields = [f[0] for f in lib.SearchArgs._fields_]
+    want = [getattr(lib.SearchArgs, f).offset for f in fields] + [ctypes.sizeof(lib.SearchArgs)]
+    assert _c_offsets("mzh_search_args", fields, tmp_path) == want
+    hdr = open(HEADER).read()
+    block = hdr[hdr.index("typedef struct mzh_search_args"):]
+    block = block[:block.index("} mzh_search_args;")]
+    n_ptr_fields = len(re.findall(r"^\s+(?:const\s+)?\w+\*\s+\w+;", block, re.M))
+    assert n_ptr_fields == 19 == len(fields) - 7
+
+
+def test_build_id_names_the_checked_out_sources(lib, tmp_path, monkeypatch):
+    """provenance: the library carries the hash of the sources + flags it was built from, equal to
+    the checked-out tree's; the hash moves with any source byte (the loader refuses a mismatch)"""
+    import shutil
+
+    from muzero_hanoi_amd import build
+
+    want = build.source_hash()
+    assert lib.build_id() == want == build.embedded_build_id(build.LIB)
+    # a copy of the tree with one changed byte hashes differently
+    csrc = tmp_path / "csrc"
+    shutil.copytree(build.CSRC, csrc)
+    with open(csrc / "mzh_tree.h", "a") as f:
+        f.write("\n")
+    monkeypatch.setattr(build, "CSRC", str(csrc))
+    assert build.source_hash() != want
+    # the GPU box runs the tree from another path: the checkout path is not part of the id
+    monkeypatch.undo()
+    assert build.source_hash([f.replace(build.REPO, "<repo>") for f in build.FLAGS]) == want
+
+
+def test_train_args_layout_matches_header(lib, tmp_path):
+    """ctypes TrainArgs == struct mzh_train_args as the C compiler lays it out"""
+    fields = [f[0] for f in lib.TrainArgs._fields_]
     want = [getattr(lib.TrainArgs, f).offset for f in fields] + [ctypes.sizeof(lib.TrainArgs)]
-    assert got == want
+    assert _c_offsets("mzh_train_args", fields, tmp_path) == want
 
 
 def test_errors_without_device_are_loud(lib):

@@ -1,7 +1,7 @@
 """World-size-2 gloo test of the sharding path on CPU: each rank searches its shard
 of the roots (the oracle stands in for the GPU search here -- the sharding, global-order draws and
-the visit all_gather are what is under test), and the gathered histograms must equal the
-single-process result bit for bit, for even and uneven shards."""
+the result all_gather are what is under test), and the gathered visit histograms, actions and
+root Q values must equal the single-process result bit for bit, for even and uneven shards."""
 import os
 import socket
 
@@ -44,9 +44,10 @@ def _worker(rank, world, port, B, out_path):
     noise, tie, u = rng.synthetic_draws(B, deterministic=False, alpha=0.25, seed=3)  # GLOBAL order
     sl = lambda x: mdist.shard(x, world, rank)
     o = orc.search(n, S, sl(obs), flat=flat, support=sup, noise=sl(noise), tie_idx=sl(tie), action_u=sl(u))
-    vis = mdist.gather_visits(torch.from_numpy(o["visits"]), B, world)
+    res = mdist.gather_results(dict(visits=torch.from_numpy(o["visits"]), action=torch.from_numpy(o["action"]),
+                                    root_q=torch.from_numpy(o["rootQ"])), B, world)
     if rank == 0:
-        np.save(out_path, vis.numpy())
+        np.savez(out_path, **{k: v.numpy() for k, v in res.items()})
     dist.destroy_process_group()
 
 
@@ -55,7 +56,7 @@ def test_sharded_equals_single(tmp_path, oracle, B):
     from muzero_hanoi_amd import distributed as mdist
     from muzero_hanoi_amd import rng
 
-    out = str(tmp_path / "vis.npy")
+    out = str(tmp_path / "res.npz")
     mp.spawn(_worker, args=(2, _free_port(), B, out), nprocs=2, join=True)
     got = np.load(out)
     w, in_dim, sup = oracle.load_weights_npz(f"{GOLDEN}/weights_N3_s0.npz")
@@ -65,5 +66,7 @@ def test_sharded_equals_single(tmp_path, oracle, B):
     obs[np.arange(B)[:, None], np.arange(3) * 3 + st] = 1
     noise, tie, u = rng.synthetic_draws(B, deterministic=False, alpha=0.25, seed=3)
     ref = oracle.search(3, 12, obs, flat=oracle.flat_weights(w), support=sup, noise=noise, tie_idx=tie, action_u=u)
-    assert np.array_equal(got, ref["visits"])
+    assert np.array_equal(got["visits"], ref["visits"])
+    assert np.array_equal(got["action"], ref["action"])
+    assert got["root_q"].dtype == np.float64 and np.array_equal(got["root_q"], ref["rootQ"])
     assert [mdist.shard_range(B, 2, r) for r in range(2)] == ([(0, 20), (20, 40)] if B == 40 else [(0, 19), (19, 37)])

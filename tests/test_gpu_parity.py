@@ -142,8 +142,62 @@ def test_mlp_batch_sizes_vs_oracle(mzh, oracle, B):
         assert np.array_equal(ri[k].cpu().numpy(), orr[k])
 
 
+def _confident_heads(oracle):
+    """weights_N4_s0 with the policy / value / reward output layers scaled (random-init logit
+    spreads ~0.2-0.5) so that most rows' logits spread beyond the softmax heads' exact-division
+    range (arguments < -65 take the IEEE fallback)"""
+    w, in_dim, sup = oracle.load_weights_npz(f"{GOLDEN}/weights_N4_s0.npz")
+    w = {k: v.copy() for k, v in w.items()}
+    for k, scale in (("policy_net.2", 250.0), ("value_net.2", 250.0), ("rwd_net.2", 500.0)):
+        w[k + ".weight"] *= np.float32(scale)
+        w[k + ".bias"] *= np.float32(scale)
+    return oracle.flat_weights(w), in_dim, sup
+
+
+def test_softmax_fallback_confident_heads_vs_oracle(mzh, oracle):
+    """A trained network's confident heads: logits more than 65 below the row maximum send the
+    softmax's division to the IEEE fallback (mzh_device.h heads).  pi, value and reward stay
+    bit-identical to the oracle for initial and recurrent inference."""
+    flat, in_dim, sup = _confident_heads(oracle)
+    B = 600
+    rs = np.random.RandomState(5)
+    x = np.zeros((B, 12), np.float32)
+    x[np.arange(B)[:, None], np.arange(4) * 3 + rs.randint(0, 3, (B, 4))] = 1
+    h = rs.uniform(0, 1, (B, 64)).astype(np.float32)
+    a = rs.randint(0, 6, B).astype(np.int32)
+    oi = oracle.initial_inference(flat, in_dim, sup, x)
+    orr = oracle.recurrent_inference(flat, in_dim, sup, h, a)
+    spread = lambda l: (l.max(1, keepdims=True) - l).max(1)
+    assert (spread(oi["value_logits"]) > 65).mean() > 0.5 and (spread(orr["reward_logits"]) > 65).mean() > 0.5
+    assert (spread(orr["policy_logits"]) > 65).any()
+    eng = _engine(mzh, 4, 4, B, 33, flat)
+    ii = eng.initial_inference(torch.tensor(x, device=DEV))
+    ri = eng.recurrent_inference(torch.tensor(h, device=DEV), torch.tensor(a, device=DEV))
+    for k in ("h", "pi", "value", "policy_logits", "value_logits"):
+        assert np.array_equal(ii[k].cpu().numpy(), oi[k]), k
+    for k in ("h", "pi", "value", "reward", "policy_logits", "value_logits", "reward_logits"):
+        assert np.array_equal(ri[k].cpu().numpy(), orr[k]), k
+
+
 # ------------------------------------------------------------------------------------ search
 KERNELS = ["coop", "wave", "wave16"]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_search_confident_heads_vs_oracle(mzh, oracle, kernel):
+    """the fused searches with confident heads (softmax IEEE fallback inside the search kernels'
+    heads) == the oracle's, every output bit for bit"""
+    flat, in_dim, sup = _confident_heads(oracle)
+    B, S, n = 300, 25, 4
+    obs, noise, tie, u = _random_search_inputs(B, n, 77)
+    eng = _engine(mzh, n, S, B, sup, flat)
+    tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
+    o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0, kernel=kernel)
+    o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+    ref = oracle.search(n, S, obs, flat=flat, support=sup, noise=noise, tie_idx=tie, action_u=u, temperature=1.0)
+    for k, rk in (("visits", "visits"), ("root_q", "rootQ"), ("action", "action"), ("sel_steps", "sel_steps"),
+                  ("extra_ties", "extra_ties")):
+        assert np.array_equal(o[k], ref[rk]), k
 
 
 def _run_replay_case(mzh, g, kernel=None):
@@ -216,10 +270,11 @@ def test_search_mlp_end_to_end_vs_oracle(mzh, oracle, case, kernel):
     assert agree.all(), f"{int(agree.sum())} / {len(agree)} histograms equal the reference's"
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("kernel,tile", [("coop", None), ("coop", 16), ("coop", 32), ("wave", None), ("wave16", None)])
 @pytest.mark.parametrize("B,S,n", [(40, 50, 4), (700, 25, 3), (9000, 8, 4), (300, 20, 7)])
-def test_search_batched_vs_oracle_random_roots(mzh, oracle, B, S, n, kernel):
-    """Ragged batches (not multiples of the 16/32-root tile), both tile sizes, vs the oracle."""
+def test_search_batched_vs_oracle_random_roots(mzh, oracle, B, S, n, kernel, tile):
+    """Ragged batches (not multiples of the 16/32-root tile), both tile sizes forced and by
+    default, vs the oracle."""
     flat, in_dim, sup = _weights(oracle, f"weights_N{n}_s0")
     rs = np.random.RandomState(B + S)
     st = rs.randint(0, 3, (B, n))
@@ -230,7 +285,8 @@ def test_search_batched_vs_oracle_random_roots(mzh, oracle, B, S, n, kernel):
     noise, tie, u = rng.synthetic_draws(B, deterministic=False, alpha=0.25, seed=B)
     eng = _engine(mzh, n, S, B, sup, flat)
     tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
-    o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0, kernel=kernel)
+    o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0, kernel=kernel,
+                   tile=tile)
     o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
     nchk = min(B, 300)
     ref = oracle.search(n, S, obs[:nchk], flat=flat, support=sup, noise=noise[:nchk], tie_idx=tie[:nchk],
@@ -276,15 +332,18 @@ def test_search_wave_equals_coop_large_batch(mzh, oracle, B, S, n, td):
     assert np.array_equal(res["wave"]["sel_steps"][idx], ref["sel_steps"])
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
-def test_search_deep_paths_replay(mzh, oracle, kernel):
-    """Replayed network outputs that drive the search down one long chain (depth >> the 16 path
-    levels cached in LDS): visits, root Q, min-max and the latent path vs the oracle."""
+@pytest.mark.parametrize("kernel,tile", [("coop", 16), ("coop", 32), ("wave", None), ("wave16", None)])
+def test_search_deep_paths_replay(mzh, oracle, kernel, tile):
+    """Replayed network outputs that drive the search down one long chain, deeper than every
+    kernel's LDS-cached path levels (wave kernels 16; cooperative 32-root tile -- the 8,192-root
+    shard of the 8-GPU headline -- 16; 16-root tile 32), so the backup's HBM branch for the deeper
+    levels (mzh_tree.h, node.py:53-70) runs on every root: visits, root Q, min-max and the latent
+    path vs the oracle."""
     B, S, n = 70, 120, 4
     g = np.random.default_rng(7)
     pi = np.full((B, S, 6), 0.002, np.float32)
     pi[:, :, 0] = 0.99
-    root_pi = np.full((B, 6), 1.0 / 6, np.float32)
+    root_pi = pi[:, 0].copy()
     value = (5.0 + g.normal(0, 0.1, (B, S))).astype(np.float32)
     rwd = g.normal(0, 0.01, (B, S)).astype(np.float32)
     rp = dict(root_pi=root_pi, pi=pi, rwd=rwd, value=value)
@@ -296,10 +355,11 @@ def test_search_deep_paths_replay(mzh, oracle, kernel):
     eng = _engine(mzh, n, S, B)
     tt = lambda a: None if a is None else torch.tensor(np.asarray(a), device=DEV)
     o = eng.search(S, replay=dict(root_pi=tt(root_pi), pi=tt(pi), reward=tt(rwd), value=tt(value)), tie_idx=tt(tie),
-                   noise=None, action_u=None, temperature=1.0, deterministic=True, kernel=kernel)
+                   noise=None, action_u=None, temperature=1.0, deterministic=True, kernel=kernel, tile=tile)
     o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
     ref = oracle.search(n, S, obs, replay=rp, tie_idx=tie, temperature=1.0, deterministic=True)
-    assert ref["latent_len"].max() > 16  # deeper than the wave kernel's LDS path cache
+    # every root's paths average deeper than any LDS path cache (max depth 120 = S)
+    assert (ref["sel_steps"] / S).min() > 32 and ref["latent_len"].max() == S
     assert np.array_equal(o["visits"], ref["visits"])
     assert np.array_equal(o["root_q"], ref["rootQ"])
     assert np.array_equal(o["minmax"][:, 0], ref["mm_max"]) and np.array_equal(o["minmax"][:, 1], ref["mm_min"])

@@ -3,7 +3,7 @@ fused search (REPLAY = false) and its replay / tree-only instantiation (REPLAY =
 rocprofv3 average duration and the per-launch PMC values, HBM bytes corrected as
 MI355X_MICROARCH.md prescribes (FETCH_SIZE x 2 on gfx950, WRITE_SIZE as is; both in KB).
 
-  python tools/traffic.py gpurun_out TAG [--traffic-json profiles/traffic_latest.json WORKLOAD]
+  python tools/traffic.py gpurun_out TAG [--traffic-json profiles/traffic_latest.json] [--config K ...]
 """
 import collections
 import csv
@@ -65,24 +65,54 @@ def summarise(root, tag):
 
 
 def main():
-    root, tag = sys.argv[1], sys.argv[2]
-    out = summarise(root, tag)
-    print(json.dumps(out, indent=1))
-    if "--traffic-json" in sys.argv:
-        i = sys.argv.index("--traffic-json")
-        path, workload = sys.argv[i + 1], sys.argv[i + 2]
-        f, t = out["fused"], out["tree"]
-        json.dump({"workload": workload, "kernel": f.get("kernel"), "avg_ns": f.get("avg_ns"),
-                   "hbm_bytes_per_launch": f.get("hbm_bytes_per_launch"),
-                   "read_bytes_corrected": f.get("hbm_read_bytes_corrected"), "write_bytes": f.get("hbm_write_bytes"),
-                   "l2_hit_rate": f.get("l2_hit_rate"), "mfma_busy_frac": f.get("mfma_busy_frac"),
-                   "clock_ghz": f.get("clock_ghz"),
-                   "tree_kernel": t.get("kernel"), "tree_avg_ns": t.get("avg_ns"),
-                   "tree_hbm_bytes_per_launch": t.get("hbm_bytes_per_launch"),
-                   "source": f"tools/prof.sh TAG={tag} + tools/traffic.py: rocprofv3 --kernel-trace --stats and separate "
-                             "--pmc passes of the bench command; FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, "
-                             "per-dispatch sums, mean over dispatches"}, open(path, "w"), indent=1)
+    """python tools/traffic.py gpurun_out TAG [--traffic-json PATH] [bench options: --config K
+    --roots-per-gpu B --kernel X --disks N --sims S]: print the summary; with --traffic-json,
+    record it under the key bench.py computes for the same options (bench.traffic_key), with the
+    build id of the library that was profiled"""
+    import argparse
 
+    sys.path.insert(0, ROOT)
+    import bench
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("tag")
+    ap.add_argument("--traffic-json", default=None)
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--roots-per-gpu", type=int, default=None)
+    ap.add_argument("--kernel", default="auto")
+    ap.add_argument("--disks", type=int, default=None)
+    ap.add_argument("--sims", type=int, default=None)
+    a = ap.parse_args()
+    out = summarise(a.root, a.tag)
+    print(json.dumps(out, indent=1))
+    if a.traffic_json:
+        from muzero_hanoi_amd import _lib
+
+        N, S, B, _ = bench.workload_shape(a.config, roots_per_gpu=a.roots_per_gpu, disks=a.disks, sims=a.sims)
+        key = bench.traffic_key(N, S, B, a.kernel)
+        f, t = out["fused"], out["tree"]
+        doc = json.load(open(a.traffic_json)) if os.path.exists(a.traffic_json) else {}
+        entries = doc.get("entries", {})
+        entries[key] = {
+            "build_id": _lib.build_id(), "kernel": f.get("kernel"), "avg_ns": f.get("avg_ns"),
+            "hbm_bytes_per_launch": f.get("hbm_bytes_per_launch"),
+            "read_bytes_corrected": f.get("hbm_read_bytes_corrected"), "write_bytes": f.get("hbm_write_bytes"),
+            "l2_hit_rate": f.get("l2_hit_rate"), "mfma_busy_frac": f.get("mfma_busy_frac"),
+            "clock_ghz": f.get("clock_ghz"),
+            "tree_kernel": t.get("kernel"), "tree_avg_ns": t.get("avg_ns"),
+            "tree_hbm_bytes_per_launch": t.get("hbm_bytes_per_launch"),
+            "tree_read_bytes_corrected": t.get("hbm_read_bytes_corrected"), "tree_write_bytes": t.get("hbm_write_bytes"),
+            "source": f"tools/prof.sh TAG={a.tag} + tools/traffic.py: rocprofv3 --kernel-trace --stats and separate "
+                      "--pmc passes of the bench command; FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, "
+                      "per-dispatch sums, mean over dispatches"}
+        json.dump({"what": "per-launch HBM bytes (PMC) of the bench workloads, keyed by bench.traffic_key; "
+                           "bench.py reports an entry only when its build_id is the running library's",
+                   "entries": entries}, open(a.traffic_json, "w"), indent=1)
+        print("recorded", key)
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 if __name__ == "__main__":
     main()
