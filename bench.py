@@ -80,6 +80,8 @@ def parse():
     p.add_argument("--no-gather", action="store_true")
     p.add_argument("--no-tree", action="store_true", help="skip the live select/backup (replay) measurement")
     p.add_argument("--kernel", choices=["auto", "coop", "wave", "wave16"], default="auto")
+    p.add_argument("--tile", type=int, choices=[16, 32], default=None,
+                   help="cooperative kernel: roots per workgroup (default by batch size)")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, one rank per GPU); gloo lets ranks share a GPU to rehearse the N>1 path")
     p.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
@@ -343,7 +345,7 @@ def main():
 
     def search():
         eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, temperature=1.0, deterministic=False,
-                   discount=0.8, eps=0.25, out=out, kernel=kern)
+                   discount=0.8, eps=0.25, out=out, kernel=kern, tile=a.tile)
 
     for _ in range(a.warmup):
         search()
@@ -382,11 +384,13 @@ def main():
                   pi=torch.from_numpy(g.dirichlet(np.full(6, 20.0), size=(B, S)).astype(np.float32)).to(dev),
                   reward=torch.from_numpy(g.normal(0, 0.05, (B, S)).astype(np.float32)).to(dev),
                   value=torch.from_numpy(g.normal(0, 0.5, (B, S)).astype(np.float32)).to(dev))
+        # the kernel's simulation-major replay records, packed once before timing (engine.pack_replay)
+        rp = dict(root_pi=rp["root_pi"], sim=engine.pack_replay(rp))
         rout = eng.alloc_search_outputs(B, S)
 
         def replay():
             eng.search(S, replay=rp, tie_idx=tie, noise=noise, action_u=u, temperature=1.0, deterministic=False,
-                       discount=0.8, eps=0.25, out=rout, kernel=kern)
+                       discount=0.8, eps=0.25, out=rout, kernel=kern, tile=a.tile)
 
         replay()
         torch.cuda.synchronize(dev)

@@ -147,9 +147,9 @@ typedef struct mzh_search_args {
   /* replay (tree-only) inputs: network outputs recorded per simulation, used instead of the MLP
    * by mzh_search_replay */
   const float* rp_root_pi; /* [B][6] */
-  const float* rp_pi;      /* [B][n_sims][6] */
-  const float* rp_reward;  /* [B][n_sims] */
-  const float* rp_value;   /* [B][n_sims] */
+  const float* rp_sim;     /* [n_sims][B][8]: simulation s of root b = its 6 priors, reward, value --
+                              simulation-major, so one simulation's reads of consecutive roots are
+                              whole cache lines (32 B per root) */
   /* outputs (visits required, others nullable) */
   int32_t* visits;      /* [B][6] root child_N (node.py:133-136) */
   double* root_q;       /* [B] root_node.Q (node.py:125-131) */

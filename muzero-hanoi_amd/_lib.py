@@ -38,7 +38,7 @@ class SearchArgs(ctypes.Structure):
         ("B", _i32), ("n_sims", _i32), ("discount", ctypes.c_double), ("eps", ctypes.c_double),
         ("temperature", ctypes.c_double), ("deterministic", _i32), ("flags", ctypes.c_uint32),
         ("obs", _vp), ("noise", _vp), ("tie_idx", _vp), ("action_u", _vp), ("minmax_in", _vp),
-        ("rp_root_pi", _vp), ("rp_pi", _vp), ("rp_reward", _vp), ("rp_value", _vp),
+        ("rp_root_pi", _vp), ("rp_sim", _vp),
         ("visits", _vp), ("root_q", _vp), ("minmax_out", _vp), ("extra_ties", _vp), ("action", _vp),
         ("pi", _vp), ("latent", _vp), ("latent_len", _vp), ("sel_steps", _vp), ("pow_table", _vp),
     ]

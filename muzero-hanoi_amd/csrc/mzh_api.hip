@@ -454,8 +454,8 @@ static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream s
   if (a->B == 0) return MZH_OK;
   if (!a->visits) return fail(MZH_ERR_ARG, "visits output is required");
   if (replay) {
-    if (!a->rp_root_pi || (a->n_sims > 0 && (!a->rp_pi || !a->rp_reward || !a->rp_value)))
-      return fail(MZH_ERR_ARG, "replay search needs rp_root_pi / rp_pi / rp_reward / rp_value");
+    if (!a->rp_root_pi || (a->n_sims > 0 && !a->rp_sim))
+      return fail(MZH_ERR_ARG, "replay search needs rp_root_pi and rp_sim");
   } else {
     if (!eng->loaded) return fail(MZH_ERR_STATE, "weights not loaded");
     if (!a->obs) return fail(MZH_ERR_ARG, "obs is required");
@@ -480,7 +480,7 @@ static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream s
   p.deterministic = a->deterministic; p.np1 = (a->flags & MZH_FLAG_NP1_UCB) ? 1 : 0;
   p.discount = a->discount; p.eps = a->eps; p.temperature = a->temperature;
   p.obs = a->obs; p.noise = a->noise; p.tie_idx = a->tie_idx; p.action_u = a->action_u; p.minmax_in = a->minmax_in;
-  p.rp_root_pi = a->rp_root_pi; p.rp_pi = a->rp_pi; p.rp_reward = a->rp_reward; p.rp_value = a->rp_value;
+  p.rp_root_pi = a->rp_root_pi; p.rp_sim = a->rp_sim;
   p.tree = eng->tree; p.htree = eng->htree; p.pathx = eng->pathx; p.table = eng->table;
   p.visits = a->visits; p.root_q = a->root_q; p.minmax_out = a->minmax_out; p.extra_ties = a->extra_ties;
   p.action = a->action; p.pi = a->pi; p.latent = a->latent; p.latent_len = a->latent_len; p.sel_steps = a->sel_steps;

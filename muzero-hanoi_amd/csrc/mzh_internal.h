@@ -17,9 +17,7 @@ struct MzhSearchParams {
   const double* action_u;
   const double* minmax_in;
   const float* rp_root_pi;
-  const float* rp_pi;
-  const float* rp_reward;
-  const float* rp_value;
+  const float* rp_sim;  // [S][B][8] replay records (6 priors, reward, value)
   unsigned char* tree;  // [B][E] MzhBlock
   float* htree;         // [B][E][64]
   uint16_t* pathx;      // [B][E] selection-path slots beyond the LDS-cached depths (wave kernel)

@@ -147,10 +147,10 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
       if (!REPLAY) {
         ho = mzh_heads_row<R, SUP33 ? 33 : 0, false>(sm, r, c, net.support, true);
       } else {
-        const size_t rs_i = (size_t)(root0 + r) * S + s;
-        ho.pp = c < MZH_A ? p.rp_pi[rs_i * MZH_A + c] : 0.0f;
-        ho.value = p.rp_value[rs_i];
-        ho.reward = p.rp_reward[rs_i];
+        const float* rec = p.rp_sim + ((size_t)s * p.B + root0 + r) * 8;  // 6 priors, reward, value
+        ho.pp = c < MZH_A ? rec[c] : 0.0f;
+        ho.reward = rec[6];
+        ho.value = rec[7];
       }
       MZH_STAMP(21);
       tree.backup(r, c, s, rs, ho.value, ho.reward, ho.pp);

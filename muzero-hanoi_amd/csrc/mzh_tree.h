@@ -54,7 +54,6 @@ struct SearchSmem {
   static constexpr int DC = DC_;
   MzhRootBlk root[R];
   MzhPathEnt pc[R][DC];
-  double bval[R][DC];  // value added at each cached path depth (backup value chain)
   double rootW[R];
   double mm[R][4];  // MinMaxStats (maximum, minimum) + normaliser (max - min, RN(1/(max - min)))
   int rootN[R];
@@ -126,7 +125,7 @@ __device__ __forceinline__ int mzh_group_pick(float ucb, int c, int lane, int ti
 
 
 // A root's search state between the tree steps, held in registers by every lane of its 8-lane group
-// (all values group-uniform; rootW is kept by lane 0, which runs the value chain).  The LDS copy
+// (all values group-uniform: every lane runs the value chain).  The LDS copy
 // (SearchSmem) is read once before the first selection and written back once for the results.
 struct MzhRootReg {
   double mmax, mmin, den, dinv;  // MinMaxStats + normaliser (mzh_mm_set)
@@ -304,15 +303,21 @@ struct MzhTree {
   }
 
   // ---------------- expand bookkeeping + backup (node.py:30-70) of simulation s ----------------
-  // Lane 0 of the root's group runs the value chain leaf -> root (two fp64 ops per level, the only
-  // serial part); the 8 lanes then update the cached path nodes in parallel and reduce the
-  // MinMaxStats candidates (max/min are exact and order-free).
+  // Every lane of the root's group runs the value chain leaf -> root (two fp64 ops per level, the
+  // only serial part) in registers, and keeps the values of the path depths j = c + 8k it updates
+  // afterwards (no LDS hand-off, no wait between the levels); the 8 lanes then update the cached
+  // path nodes in parallel and reduce the MinMaxStats candidates (max/min are exact and order-free).
   // val / rew: the new node's value and reward (every lane), pp: lane c's child prior
   __device__ __forceinline__ void backup(const int r, const int c, const int s, MzhRootReg& rs, float val, float rew,
                                          float pp) {
     MzhBlock* tb = reinterpret_cast<MzhBlock*>(p.tree) + (size_t)(root0 + r) * p.E;
     MzhRootBlk& rb = st.root[r];
     const int enew = s + 1;
+    constexpr int NB = DC / 8;  // cached depths per lane
+    // the reward snapshots of the cached depths, read before anything else (independent of the chain)
+    float Rj[DC];
+#pragma unroll
+    for (int jj = 0; jj < DC; ++jj) Rj[jj] = st.pc[r][jj].R;
     MZH_STAMP_DECL
     if (!REPLAY) {
       // the new node's latent (read back when one of its children is expanded -- usually
@@ -341,66 +346,71 @@ struct MzhTree {
         tb[le].sl[la].nx.X = (int16_t)enew;
         tb[le].sl[la].R = rew;
       }
-      double v = (double)val;
-      int j = depth - 1;
-      for (; j >= DC; --j) {  // beyond the LDS path cache (rare): update here from HBM
-        const int slot = path[r * PL + j];
-        const int e = slot >> 3, a = slot & 7;
-        const double rw = (j == depth - 1) ? (double)rew : (double)tb[e].sl[a].R;
-        const double W = tb[e].W[a] + v;
-        const int N = tb[e].sl[a].nx.N + 1;
-        tb[e].W[a] = W;
-        tb[e].sl[a].nx.N = (uint16_t)N;
+    }
+    double v = (double)val;
+    int j = depth - 1;
+    for (; j >= DC; --j) {  // beyond the LDS path cache (rare): lane j % 8 updates depth j from HBM
+      const int slot = path[r * PL + j];
+      const int e = slot >> 3, a = slot & 7;
+      MzhBlock* eb = tb + e;
+      const double rw = (j == depth - 1) ? (double)rew : (double)eb->sl[a].R;
+      if (c == (j & 7)) {
+        const double W = eb->W[a] + v;
+        const int N = eb->sl[a].nx.N + 1;
+        eb->W[a] = W;
+        eb->sl[a].nx.N = (uint16_t)N;
         const double q = rw + disc * mzh_div(W, (double)N, inv[N]);
         lmax = q > lmax ? q : lmax;
         lmin = q < lmin ? q : lmin;
-        v = rw + disc * v;
       }
-      // the LDS-cached depths j <= jtop: every reward snapshot is read up front, then the fp64
-      // chain runs in registers (the leaf takes its new reward); a step above this lane's jtop
-      // keeps v, and steps above every active lane's jtop are skipped (wave-uniform branch).
-      // bval entries at depths >= `depth` are written but never read.
-      const int jtop = j;
-      float Rj[DC];
+      v = rw + disc * v;
+    }
+    // the cached depths j <= jtop: the fp64 chain in registers (the leaf takes its new reward); a
+    // step above this lane's jtop keeps v, and steps above every active lane's jtop are skipped
+    // (wave-uniform branch).  bv[k] = the value added at depth c + 8k.
+    const int jtop = j;
+    double bv[NB];
 #pragma unroll
-      for (int jj = 0; jj < DC; ++jj) Rj[jj] = st.pc[r][jj].R;
+    for (int k = 0; k < NB; ++k) bv[k] = 0.0;
 #pragma unroll
-      for (int jj = DC - 1; jj >= 0; --jj) {
-        if (!__any(jj <= jtop)) continue;
-        st.bval[r][jj] = v;
-        const double rw = jj == depth - 1 ? (double)rew : (double)Rj[jj];
-        const double vn = rw + disc * v;
-        v = jj <= jtop ? vn : v;
-      }
+    for (int jj = DC - 1; jj >= 0; --jj) {
+      if (!__any(jj <= jtop)) continue;
+      if ((jj & 7) == c) bv[jj >> 3] = v;
+      const double rw = jj == depth - 1 ? (double)rew : (double)Rj[jj];
+      const double vn = rw + disc * v;
+      v = jj <= jtop ? vn : v;
+    }
+    {  // the root (rwd = 0.0): every lane holds the same rootW
       const double W = rs.rootW + v;
       const int N = rs.rootN + 1;
       rs.rootW = W;
-      const double q = 0.0 + disc * mzh_div(W, (double)N, inv[N]);  // root rwd = 0.0
+      const double q = 0.0 + disc * mzh_div(W, (double)N, inv[N]);
       lmax = q > lmax ? q : lmax;
       lmin = q < lmin ? q : lmin;
     }
     MZH_STAMP(17);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int jmax = depth < DC ? depth : DC;
-    for (int j = c; j < jmax; j += 8) {
-      const int slot = path[r * PL + j];
-      const int e = slot >> 3, a = slot & 7;
-      const MzhPathEnt pe = st.pc[r][j];
-      const double rw = (j == depth - 1) ? (double)rew : (double)pe.R;
-      const double W = pe.W + st.bval[r][j];
-      const int N = pe.N + 1;
-      if (e == 0) {
-        rb.W[a] = W;
-        rb.N[a] = N;
-      } else {
-        tb[e].W[a] = W;
-        tb[e].sl[a].nx.N = (uint16_t)N;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int jp = c + 8 * k;
+      if (jp < jmax) {
+        const int slot = path[r * PL + jp];
+        const int e = slot >> 3, a = slot & 7;
+        const MzhPathEnt pe = st.pc[r][jp];
+        const double rw = (jp == depth - 1) ? (double)rew : (double)pe.R;
+        const double W = pe.W + bv[k];
+        const int N = pe.N + 1;
+        if (e == 0) {
+          rb.W[a] = W;
+          rb.N[a] = N;
+        } else {
+          tb[e].W[a] = W;
+          tb[e].sl[a].nx.N = (uint16_t)N;
+        }
+        const double q = rw + disc * mzh_div(W, (double)N, inv[N]);
+        lmax = q > lmax ? q : lmax;
+        lmin = q < lmin ? q : lmin;
       }
-      const double q = rw + disc * mzh_div(W, (double)N, inv[N]);
-      lmax = q > lmax ? q : lmax;
-      lmin = q < lmin ? q : lmin;
     }
     MZH_STAMP(18);
     rs.rootN += 1;

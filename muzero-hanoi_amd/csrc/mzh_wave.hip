@@ -696,23 +696,31 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
   // the new node's block, then backup (node.py:30-70)
   auto phase_head = [&](int s) {
     if (!REPLAY) {
-      // the new node's 6 children (node.py:44-49): lane groups 0/1 hold pi[0..3] / pi[4..5]
-      if (g < 2) {
+      // the new node's 6 children (node.py:44-49): N = 0, X = -1, R = 0, P, W = 0.  The whole 128-B
+      // line as eight 16-B stores, two per lane group (lane groups 0/1 hold pi[0..3] / pi[4..5]):
+      // a line written whole is valid in L2 without a fill from HBM.  Chunk k = bytes 16k..16k+15:
+      // 0 nx0-3 | 1 nx4,5 R0,1 | 2 R2-5 | 3 P0-3 | 4 P4,5 W0 | 5 W1,2 | 6 W3,4 | 7 W5 pad
 #pragma unroll
-        for (int n = 0; n < NT; ++n) {
-          if (!cvalid[n]) continue;
-          MzwBlock* nb = reinterpret_cast<MzwBlock*>(p.tree) + (size_t)croot[n] * E + s + 1;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int c = 4 * g + i;
-            if (c < MZH_A) {
-              *reinterpret_cast<uint32_t*>(&nb->nx[c]) = 0xFFFF0000u;  // N = 0, X = -1
-              nb->R[c] = 0.0f;
-              nb->P[c] = cpi[n][i];
-              nb->W[c] = 0.0;
-            }
-          }
+      for (int n = 0; n < NT; ++n) {
+        if (!cvalid[n]) continue;
+        uint4* nb = reinterpret_cast<uint4*>(reinterpret_cast<MzwBlock*>(p.tree) + (size_t)croot[n] * E + s + 1);
+        const uint32_t nx = 0xFFFF0000u;  // N = 0, X = -1
+        uint4 c0, c1;
+        if (g == 0) {
+          c0 = make_uint4(nx, nx, nx, nx);
+          c1 = make_uint4(__float_as_uint(cpi[n][0]), __float_as_uint(cpi[n][1]), __float_as_uint(cpi[n][2]),
+                          __float_as_uint(cpi[n][3]));
+        } else if (g == 1) {
+          c0 = make_uint4(nx, nx, 0u, 0u);
+          c1 = make_uint4(__float_as_uint(cpi[n][0]), __float_as_uint(cpi[n][1]), 0u, 0u);
+        } else {
+          c0 = make_uint4(0u, 0u, 0u, 0u);
+          c1 = c0;
         }
+        // g0: chunks 0, 3; g1: chunks 1, 4; g2: chunks 2, 5; g3: chunks 6, 7
+        const int k0 = g < 3 ? g : 6, k1 = g < 3 ? g + 3 : 7;
+        nb[k0] = c0;
+        nb[k1] = c1;
       }
     }
     // ---------------- expand bookkeeping + backup (node.py:30-70): one lane per root ----------------
@@ -720,16 +728,22 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
       const int enew = s + 1;
       float vv, rr;
       if (REPLAY) {
-        vv = p.rp_value[(size_t)rroot * S + s];
-        rr = p.rp_reward[(size_t)rroot * S + s];
-        MzwBlock* nb = &tb[enew];
-#pragma unroll
-        for (int c = 0; c < MZH_A; ++c) {
-          *reinterpret_cast<uint32_t*>(&nb->nx[c]) = 0xFFFF0000u;
-          nb->R[c] = 0.0f;
-          nb->P[c] = p.rp_pi[((size_t)rroot * S + s) * MZH_A + c];
-          nb->W[c] = 0.0;
-        }
+        const uint4* rec = reinterpret_cast<const uint4*>(p.rp_sim + ((size_t)s * p.B + rroot) * 8);
+        const uint4 r0 = rec[0], r1 = rec[1];  // priors 0-3 | priors 4, 5, reward, value
+        rr = __uint_as_float(r1.z);
+        vv = __uint_as_float(r1.w);
+        // the whole 128-B line as eight 16-B stores (see phase_head's fused form)
+        uint4* nb = reinterpret_cast<uint4*>(&tb[enew]);
+        const uint32_t nx = 0xFFFF0000u;
+        const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+        nb[0] = make_uint4(nx, nx, nx, nx);
+        nb[1] = make_uint4(nx, nx, 0u, 0u);
+        nb[2] = z;
+        nb[3] = r0;
+        nb[4] = make_uint4(r1.x, r1.y, 0u, 0u);
+        nb[5] = z;
+        nb[6] = z;
+        nb[7] = z;
       } else {
         // root lane rho is column rho & 15 of tile rho >> 4 (every row of a column holds its scalars)
         vv = val[0];

@@ -176,9 +176,7 @@ class Engine:
         a.minmax_in = ptr(dev(minmax_in, torch.float64))
         if replay is not None:
             a.rp_root_pi = ptr(dev(replay["root_pi"], torch.float32))
-            a.rp_pi = ptr(dev(replay["pi"], torch.float32))
-            a.rp_reward = ptr(dev(replay["reward"], torch.float32))
-            a.rp_value = ptr(dev(replay["value"], torch.float32))
+            a.rp_sim = ptr(dev(replay["sim"] if "sim" in replay else pack_replay(replay), torch.float32))
         a.visits = ptr(out["visits"])
         a.root_q = ptr(out.get("root_q"))
         a.minmax_out = ptr(out.get("minmax"))
@@ -197,6 +195,15 @@ class Engine:
         check(fn(self._h, ctypes.byref(a), self._stream()), "mzh_search")
         out["_keep"] = keep  # inputs stay alive until the caller is done with the async call
         return out
+
+
+def pack_replay(replay):
+    """recorded network outputs pi [B,S,6], reward [B,S], value [B,S] -> the kernel's replay records
+    [S,B,8] (6 priors, reward, value per simulation and root; simulation-major, mzh_search_args.rp_sim)"""
+    pi = torch.as_tensor(replay["pi"], dtype=torch.float32)
+    rw = torch.as_tensor(replay["reward"], dtype=torch.float32).to(pi.device)
+    va = torch.as_tensor(replay["value"], dtype=torch.float32).to(pi.device)
+    return torch.cat([pi, rw[..., None], va[..., None]], -1).transpose(0, 1).contiguous()
 
 
 # ---------------------------------------------------------------- environment (no engine needed)

@@ -25,6 +25,7 @@ SEARCH = {16: "backup:latent+new-block stores", 17: "backup:value chain (lane 0)
 
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+    replay = "--replay" in sys.argv
     S = 50
     torch.manual_seed(0)
     net = MuZeroNet(12, 6, 0.002, "cpu", TD_return=True)
@@ -49,10 +50,18 @@ def main():
     from bench import random_roots
     obs = torch.from_numpy(random_roots(4, B, 1)).cuda()
     noise, tie, u = (torch.from_numpy(x).cuda() for x in rng.synthetic_draws(B, deterministic=False, alpha=0.25, seed=1))
-    eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u)
+    rp = None
+    if replay:  # network outputs drawn like bench.py's tree measurement
+        g = np.random.default_rng(7)
+        rp = dict(root_pi=torch.from_numpy(g.dirichlet(np.full(6, 20.0), size=B).astype(np.float32)).cuda(),
+                  pi=torch.from_numpy(g.dirichlet(np.full(6, 20.0), size=(B, S)).astype(np.float32)).cuda(),
+                  reward=torch.from_numpy(g.normal(0, 0.05, (B, S)).astype(np.float32)).cuda(),
+                  value=torch.from_numpy(g.normal(0, 0.5, (B, S)).astype(np.float32)).cuda())
+    run = lambda: eng.search(S, obs=None if replay else obs, replay=rp, tie_idx=tie, noise=noise, action_u=u)
+    run()
     torch.cuda.synchronize()
     L.mzh_diag_stamps(buf.ctypes.data)
-    eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u)
+    run()
     torch.cuda.synchronize()
     L.mzh_diag_stamps(buf.ctypes.data)
     per = buf / S
