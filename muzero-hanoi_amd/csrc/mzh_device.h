@@ -23,6 +23,12 @@
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+// a compile-time bool carried by value (selects a specialised copy of a generic lambda)
+template <bool B>
+struct MzhBool {
+  static constexpr bool value = B;
+};
+
 // ------------------------------------------------------------------------------------------
 // Diagnostic phase stamps (only in the -DMZH_STAMPS build, libmzh_diag.so; never in libmzh.so).
 // Lane 0 of every wave accumulates s_memtime deltas per phase into mzh_stamp_acc[wave][phase].

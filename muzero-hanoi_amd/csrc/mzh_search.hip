@@ -28,7 +28,9 @@
 template <int R>
 constexpr int search_dc() { return R == 32 ? 16 : 32; }  // LDS-cached path depths
 
-template <int R, bool REPLAY, bool OHL, bool SUP33>
+// MMIN: the launch has caller-given MinMaxStats bounds (p.minmax_in), which could make max - min
+// subnormal: the selection then checks for that (MzhTree::select)
+template <int R, bool REPLAY, bool OHL, bool SUP33, bool MMIN>
 __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, MzhSearchParams p) {
   constexpr int DC = search_dc<R>();
   using Smem = SearchSmem<R, DC>;
@@ -131,7 +133,7 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
   if (town) rs.load(st, tr);
 
   MZH_STAMP_DECL
-  if (town) tree.select(tr, tc, 0, rs);
+  if (town) tree.template select<MMIN>(tr, tc, 0, rs);
   __syncthreads();
   for (int s = 0; s < S; ++s) {
     // ---------------- expand via the network (mcts.py:88-106) ----------------
@@ -157,7 +159,7 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
       MZH_STAMP(22);
       if (s + 1 < S) {
         group_sync();
-        tree.select(r, c, s + 1, rs);
+        tree.template select<MMIN>(r, c, s + 1, rs);
         MZH_STAMP(30);
       }
     }
@@ -222,15 +224,25 @@ static size_t search_smem_bytes(int S, bool ohl) {
   return (b + 15) & ~(size_t)15;
 }
 
-template <int R, bool REPLAY, bool OHL, bool SUP33>
-static hipError_t launch_search_s(const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
+template <int R, bool REPLAY, bool OHL, bool SUP33, bool MMIN>
+static hipError_t launch_search_m(const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
   const size_t smem = search_smem_bytes<R>(p.S, OHL);
-  const void* fn = reinterpret_cast<const void*>(&mzh_search_kernel<R, REPLAY, OHL, SUP33>);
+  const void* fn = reinterpret_cast<const void*>(&mzh_search_kernel<R, REPLAY, OHL, SUP33, MMIN>);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
   const int grid = (p.B + R - 1) / R;
-  hipLaunchKernelGGL((mzh_search_kernel<R, REPLAY, OHL, SUP33>), dim3(grid), dim3(MZH_THREADS), smem, stream, net, p);
+  hipLaunchKernelGGL((mzh_search_kernel<R, REPLAY, OHL, SUP33, MMIN>), dim3(grid), dim3(MZH_THREADS), smem, stream, net,
+                     p);
   return hipGetLastError();
+}
+template <int R, bool REPLAY, bool OHL, bool SUP33>
+static hipError_t launch_search_s(const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
+  // caller-given bounds: the instantiation that checks for a subnormal max - min (never with OHL: the
+  // one-hot table is only an LDS placement choice of the 32-root tile)
+  if constexpr (!OHL) {
+    if (p.minmax_in) return launch_search_m<R, REPLAY, OHL, SUP33, true>(net, p, stream);
+  }
+  return launch_search_m<R, REPLAY, OHL, SUP33, false>(net, p, stream);
 }
 template <int R, bool REPLAY, bool OHL>
 static hipError_t launch_search_t(const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
@@ -247,7 +259,7 @@ size_t mzh_search_smem_bytes(int R, int S) { return R == 32 ? search_smem_bytes<
 hipError_t mzh_launch_search(int R, bool replay, const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
   if (R == 32) {
     if (replay) return launch_search_t<32, true, false>(net, p, stream);
-    if (search_smem_bytes<32>(p.S, true) <= kLdsBytes) return launch_search_t<32, false, true>(net, p, stream);
+    if (search_smem_bytes<32>(p.S, true) <= kLdsBytes && !p.minmax_in) return launch_search_t<32, false, true>(net, p, stream);
     return launch_search_t<32, false, false>(net, p, stream);
   }
   return replay ? launch_search_t<16, true, false>(net, p, stream) : launch_search_t<16, false, false>(net, p, stream);

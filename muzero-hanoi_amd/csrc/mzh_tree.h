@@ -76,9 +76,16 @@ __device__ __forceinline__ double mzh_div(double a, double b, double y) {
   return __builtin_fma(r, y, q);
 }
 
-// MinMaxStats.normalize (utils_mcts.py:12-16) with den = max - min, dinv = RN(1/den)
-__device__ __forceinline__ double mzh_normalize(double v, bool has, double mn, double den, double dinv) {
-  return has ? mzh_div(v - mn, den, dinv) : v;
+// MinMaxStats.normalize (utils_mcts.py:12-16) with den = max - min, dinv = RN(1/den).  The
+// Markstein quotient needs a normal den (its reciprocal finite, the residual exact); `exact`
+// (wave-uniform: some lane of the wave has a subnormal den -- only reachable from caller-given
+// MinMaxStats bounds, never from fp32 network outputs) takes the IEEE division instead
+__device__ __forceinline__ double mzh_normalize(double v, bool has, double mn, double den, double dinv, bool exact) {
+  return has ? (exact ? (v - mn) / den : mzh_div(v - mn, den, dinv)) : v;
+}
+// whether any lane of the wave needs the exact normaliser (a non-zero subnormal max - min)
+__device__ __forceinline__ bool mzh_need_exact(bool has, double den) {
+  return __builtin_amdgcn_ballot_w64(has && !(den >= 2.2250738585072014e-308)) != 0;
 }
 
 // ucb = fl32(Q) + fl32(U) for one child (node.py:90-123); `tnp` = table[N_parent], inv[k] = RN(1/k)
@@ -86,9 +93,9 @@ __device__ __forceinline__ double mzh_normalize(double v, bool has, double mn, d
 // by side; for Nc = 0 the Q chain computes from inv[0] = inf and its result is discarded.
 __device__ __forceinline__ float mzh_ucb(int Nc, double Wc, float Rc, double P64, bool p64_semantics, double tnp,
                                          double disc, bool has, double mn, double den, double dinv,
-                                         const double* inv) {
+                                         const double* inv, bool exact) {
   const double i0 = inv[Nc], i1 = inv[Nc + 1];
-  const double qn = mzh_normalize((double)Rc + disc * mzh_div(Wc, (double)Nc, i0), has, mn, den, dinv);
+  const double qn = mzh_normalize((double)Rc + disc * mzh_div(Wc, (double)Nc, i0), has, mn, den, dinv, exact);
   const float q32 = Nc > 0 ? (float)qn : 0.0f;
   const double w = mzh_div(tnp, (double)(Nc + 1), i1);
   // np.float64 priors (Dirichlet-mixed root) or NumPy-1 promotion: fl32(fl64(prior * w));
@@ -181,10 +188,25 @@ struct MzhTree {
   double disc;
   bool noised;
 
+  // MMIN (the launch has caller-given MinMaxStats bounds): a wave with a root whose max - min is a
+  // non-zero subnormal takes the exact-normaliser copy, chosen once per selection.  Without caller
+  // bounds max - min is never subnormal (fresh bounds are +-inf; q values built from fp32 network
+  // outputs are 0 or larger than 1e-70, so two distinct ones differ by far more than 2^-1022), and
+  // the kernel carries only the Markstein copy.
+  template <bool MMIN>
   __device__ __forceinline__ void select(const int r, const int c, const int s, MzhRootReg& rs) {
+    if (MMIN && __builtin_expect(mzh_need_exact(rs.mmax > rs.mmin, rs.den), 0))
+      select_impl<true>(r, c, s, rs);
+    else
+      select_impl<false>(r, c, s, rs);
+  }
+
+  template <bool EXACT>
+  __device__ __forceinline__ void select_impl(const int r, const int c, const int s, MzhRootReg& rs) {
     const MzhBlock* tb = reinterpret_cast<const MzhBlock*>(p.tree) + (size_t)(root0 + r) * p.E;
     const double mmax = rs.mmax, mmin = rs.mmin, den = rs.den, dinv = rs.dinv;
     const bool has = mmax > mmin;
+    constexpr bool exact = EXACT;
     int firstTie = rs.firstTie;
     int extra = rs.extra;
     const int tie = rs.tie;
@@ -204,7 +226,7 @@ struct MzhTree {
       Xc = rb.X[c];
       Wc = rb.W[c];
       Rc = rb.R[c];
-      const float u = mzh_ucb(Nc, Wc, Rc, rb.P64[c], noised || p.np1, table[rs.rootN], disc, has, mmin, den, dinv, inv);
+      const float u = mzh_ucb(Nc, Wc, Rc, rb.P64[c], noised || p.np1, table[rs.rootN], disc, has, mmin, den, dinv, inv, exact);
       ucb = c < MZH_A ? u : -__builtin_inff();
     }
     int pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
@@ -252,7 +274,7 @@ struct MzhTree {
       pf0 = *reinterpret_cast<const int*>(tb + (xc >= 0 ? xc : e));
       Nc = nxc & 0xFFFF;
       {
-        const float u = mzh_ucb(Nc, Wc, Rc, (double)Pc, p.np1, tnp, disc, has, mmin, den, dinv, inv);
+        const float u = mzh_ucb(Nc, Wc, Rc, (double)Pc, p.np1, tnp, disc, has, mmin, den, dinv, inv, exact);
         ucb = c < MZH_A ? u : -__builtin_inff();
       }
 #ifdef MZH_STAMPS

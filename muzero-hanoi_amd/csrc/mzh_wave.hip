@@ -321,12 +321,13 @@ __device__ __forceinline__ double mzw_div(double a, double b, double y) {
 // ucb = fl32(Q) + fl32(U) for one child (node.py:90-123); inv[k] = RN(1/k) (LDS table)
 __device__ __forceinline__ float mzw_ucb(int Nc, double Wc, float Rc, double P64, bool p64_semantics, double tnp,
                                          double disc, bool has, double mn, double den, double dinv,
-                                         const double* inv) {
+                                         const double* inv, bool exact) {
   // branch-free: both reciprocals in one LDS read, the Q and U chains side by side (for Nc = 0 the
   // Q chain runs on inv[0] = inf and is discarded)
   const double i0 = inv[Nc], i1 = inv[Nc + 1];
   const double v = (double)Rc + disc * mzw_div(Wc, (double)Nc, i0);
-  const double qn = has ? mzw_div(v - mn, den, dinv) : v;
+  // exact (wave-uniform): IEEE division for a subnormal den (see mzh_tree.h mzh_normalize)
+  const double qn = has ? (exact ? (v - mn) / den : mzw_div(v - mn, den, dinv)) : v;
   const float q32 = Nc > 0 ? (float)qn : 0.0f;
   const double w = mzw_div(tnp, (double)(Nc + 1), i1);
   const float u32 = p64_semantics ? (float)(P64 * w) : (float)P64 * (float)w;
@@ -488,8 +489,11 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
   floatx4 cpi[NT];
 
   // select one leaf per root, then hand its parent latent index / move to the column lanes
-  auto phase_select = [&](int s) {
+  // ex: MzhBool<true> = the exact (IEEE-division) normaliser, for a wave where some root's max - min
+  // is a non-zero subnormal (caller-given bounds only); chosen once per selection
+  auto phase_select = [&](int s, auto ex) {
     (void)s;
+    constexpr bool exact = decltype(ex)::value;
     // ---------------- select (mcts.py:75-86; node.py:72-123): one lane per root ----------------
     if (rvalid) {
       const bool has = mmax > mmin;
@@ -499,7 +503,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
       for (int j = 0; j < 3; ++j) {
         const int c = 3 * half + j;
         u[j] = mzw_ucb(ws.rN[c][rho], ws.rW[c][rho], ws.rR[c][rho], ws.rP[c][rho], noised || p.np1, tr, disc, has,
-                       mmin, den, dinv, inv);
+                       mmin, den, dinv, inv, exact);
       }
       int pick = mzw_pick_pair(u, half, tie, firstTie, extra);
       int Np = ws.rN[pick][rho], X = ws.rX[pick][rho];
@@ -546,7 +550,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
           }
           const double tn = table[Np];
   #pragma unroll
-          for (int j = 0; j < 3; ++j) u[j] = mzw_ucb(hn[j] & 0xFFFF, hw[j], hr[j], (double)hp[j], p.np1, tn, disc, has, mmin, den, dinv, inv);
+          for (int j = 0; j < 3; ++j) u[j] = mzw_ucb(hn[j] & 0xFFFF, hw[j], hr[j], (double)hp[j], p.np1, tn, disc, has, mmin, den, dinv, inv, exact);
           pick = mzw_pick_pair(u, half, tie, firstTie, extra);
           // this lane's candidate for the picked slot (valid on the owning half), then the owner's copy
           const int jl = pick - 3 * half;
@@ -604,7 +608,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
             const float Rj = half ? Rc[3 + j] : Rc[j];
             const double Wj = half ? Wc[3 + j] : Wc[j];
             const float Pj = __int_as_float(half ? dw[15 + j] : dw[12 + j]);
-            u[j] = mzw_ucb(nxj & 0xFFFF, Wj, Rj, (double)Pj, p.np1, tn, disc, has, mmin, den, dinv, inv);
+            u[j] = mzw_ucb(nxj & 0xFFFF, Wj, Rj, (double)Pj, p.np1, tn, disc, has, mmin, den, dinv, inv, exact);
           }
           pick = mzw_pick_pair(u, half, tie, firstTie, extra);
           nx = dw[0];
@@ -825,7 +829,10 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
   MZH_STAMP_DECL
   for (int s = 0; s < S; ++s) {
     MZH_STAMP(4);
-    phase_select(s);
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(rvalid && mmax > mmin && !(den >= 2.2250738585072014e-308)) != 0, 0))
+      phase_select(s, MzhBool<true>{});
+    else
+      phase_select(s, MzhBool<false>{});
     MZH_STAMP(0);
     // a wave in its matrix phase wins VALU issue arbitration over the co-resident wave's tree work
     __builtin_amdgcn_s_setprio(1);

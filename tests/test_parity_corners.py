@@ -313,3 +313,35 @@ def test_random_reset_dropin():
         assert state_index(env.c_state) == want
         assert obs.sum() == int(n) and obs.dtype == np.float64
     assert np.array_equal(np.random.random_sample(4), g["post_rng"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel,tile", [("coop", 16), ("coop", 32), ("wave", None), ("wave16", None)])
+def test_subnormal_minmax_gap(oracle, kernel, tile):
+    """MinMaxStats bounds whose difference is a non-zero subnormal (reachable only from caller-given
+    bounds: q values built from fp32 network outputs never get that close) make RN(1/(max - min))
+    overflow; the kernels then normalise with the IEEE division (utils_mcts.py:12-16) instead of the
+    Markstein quotient, and equal the oracle's exact arithmetic"""
+    import torch
+
+    from muzero_hanoi_amd.engine import Engine
+
+    B, S, n = 40, 20, 4
+    g = np.random.default_rng(5)
+    rp = dict(root_pi=g.dirichlet(np.full(6, 1.0), size=B).astype(np.float32),
+              pi=g.dirichlet(np.full(6, 1.0), size=(B, S)).astype(np.float32),
+              rwd=np.zeros((B, S), np.float32), value=np.zeros((B, S), np.float32))
+    mm = np.tile(np.array([[3e-310, 1e-310]]), (B, 1))
+    tie = g.integers(0, 6, B).astype(np.int32)
+    obs = np.zeros((B, 3 * n), np.float32)
+    ref = oracle.search(n, S, obs, replay=rp, tie_idx=tie, temperature=1.0, deterministic=True, minmax_in=mm)
+    assert ref["mm_max"][0] == 3e-310 and ref["mm_min"][0] == 0.0  # the gap stays subnormal
+    eng = Engine(n, S, B, 33)
+    tt = lambda a: torch.tensor(np.asarray(a), device="cuda")
+    o = eng.search(S, replay=dict(root_pi=tt(rp["root_pi"]), pi=tt(rp["pi"]), reward=tt(rp["rwd"]),
+                                  value=tt(rp["value"])), tie_idx=tt(tie), minmax_in=tt(mm), temperature=1.0,
+                   deterministic=True, kernel=kernel, tile=tile)
+    assert np.array_equal(o["visits"].cpu().numpy(), ref["visits"])
+    assert np.array_equal(o["root_q"].cpu().numpy(), ref["rootQ"])
+    assert np.array_equal(o["minmax"].cpu().numpy()[:, 0], ref["mm_max"])
+    assert np.array_equal(o["sel_steps"].cpu().numpy(), ref["sel_steps"])
