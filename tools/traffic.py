@@ -109,7 +109,7 @@ def main():
         json.dump({"what": "per-launch HBM bytes (PMC) of the bench workloads, keyed by bench.traffic_key; "
                            "bench.py reports an entry only when its build_id is the running library's",
                    "entries": entries}, open(a.traffic_json, "w"), indent=1)
-        print("recorded", key)
+        print("recorded", key, file=sys.stderr)
 
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
