@@ -4,7 +4,7 @@ Roots are independent, so the search shards with no data-path collective: rank r
 contiguous slice [r*B/W, (r+1)*B/W) of the global batch.  Every random draw is made for the
 GLOBAL batch in global root order and then sliced, so results do not depend on the world size.
 The single exchange is one all_gather of each root's search result -- what run_mcts returns
-(MCTS/mcts.py:122-126): the visit histogram, the action and root Q (fp64) -- packed as 9 int32
+(MCTS/mcts.py:122-126): the visit histogram, the action and root Q (fp64) -- packed as 10 int32
 words per root (RCCL over xGMI on the GPUs, gloo in the CPU tests); weights are broadcast once
 at start-up.
 """
@@ -35,12 +35,16 @@ def broadcast_weights(flat, device, src=0):
 
 
 def gather_rows(local, B, world):
-    """all_gather of per-rank [b_r, k] rows -> global [B, k] in root order.  Shards may differ by
-    one root: each rank pads to the largest shard size."""
+    """all_gather of per-rank [b_r, k] rows -> global [B, k] in root order.  Even shards (every
+    BASELINE config at N = 1, 2, 4, 8) gather straight into the result; uneven ones (they differ by
+    one root) pad to the largest shard and drop the padding rows afterwards."""
     bmax = shard_range(B, world, 0)[1]  # rank 0 holds the largest shard
+    out = torch.empty((world * bmax, local.shape[1]), dtype=local.dtype, device=local.device)
+    if B % world == 0:
+        dist.all_gather_into_tensor(out, local.contiguous())
+        return out
     pad = torch.zeros((bmax, local.shape[1]), dtype=local.dtype, device=local.device)
     pad[: local.shape[0]] = local
-    out = torch.empty((world * bmax, local.shape[1]), dtype=local.dtype, device=local.device)
     dist.all_gather_into_tensor(out, pad)
     parts = []
     for r in range(world):
@@ -54,17 +58,23 @@ def gather_visits(local, B, world):
     return gather_rows(local, B, world)
 
 
+# packed result row: visits (6 int32), action (1), pad (1), root Q's fp64 bits (2) -- 40 B, so root Q
+# sits 8-byte aligned in every row and the unpacked fields are views of the gathered rows
+PACK_WORDS = 10
+
+
 def pack_results(visits, action, root_q):
-    """[b, 9] int32: visits (6), action (1), root Q's fp64 bits (2) -- one collective per search"""
+    """[b, 10] int32 rows for one collective per search (see PACK_WORDS)"""
     b = visits.shape[0]
     return torch.cat([visits.to(torch.int32).reshape(b, 6), action.to(torch.int32).reshape(b, 1),
+                      torch.zeros((b, 1), dtype=torch.int32, device=visits.device),
                       root_q.to(torch.float64).contiguous().view(torch.int32).reshape(b, 2)], 1)
 
 
 def unpack_results(packed):
+    """views of the gathered rows (no copies): visits [B, 6], action [B], root_q [B] fp64"""
     b = packed.shape[0]
-    return dict(visits=packed[:, :6].contiguous(), action=packed[:, 6].contiguous(),
-                root_q=packed[:, 7:9].contiguous().view(torch.float64).reshape(b))
+    return dict(visits=packed[:, :6], action=packed[:, 6], root_q=packed[:, 8:10].view(torch.float64).reshape(b))
 
 
 def gather_results(out, B, world):
