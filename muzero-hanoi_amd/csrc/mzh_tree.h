@@ -230,23 +230,35 @@ struct MzhTree {
       ucb = c < MZH_A ? u : -__builtin_inff();
     }
     int pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
-    // the picking lane records the path entry and its own statistics; the packed (N | X << 16)
-    // word of the pick, taken over the group's DPP tree, moves the selection on
-    if (c == pick) {
-      path[r * PL] = (uint16_t)pick;
-      st.pc[r][0] = MzhPathEnt{Wc, Rc, Nc};
-    }
     // every lane prefetches its own child's block (the selection's next level is one of
     // them): the block's cache lines are in flight while this level's UCB/argmax completes
     // (unconditional loads -- a lane without a child re-reads a valid block -- so the
     // compiler can count outstanding loads and wait only for the ones a level needs)
     int pf0 = *reinterpret_cast<const int*>(tb + (Xc >= 0 ? Xc : 0));
+    // the packed (N | X << 16) word of the pick, taken over the group's DPP tree, moves the selection on
     int nx = mzh_group_take((Nc & 0xFFFF) | (Xc << 16), c == pick);
     int depth = 1, e = 0;
 
     // deeper levels: tree blocks in HBM (L2); lanes 6, 7 re-read slot 5 and act as
-    // unexpanded, unvisited pads (N = 0, X = -1)
+    // unexpanded, unvisited pads (N = 0, X = -1).  PIPE (16-root tiles): a level's block loads are
+    // issued as soon as its block is known -- before the previous level's path stores, which then
+    // run under their latency (the loads after the last level re-read the leaf's block, unused):
+    // 4,096 roots -1.0%; the 32-root tile +0.4%, so it loads each level's block at the level's top
+    constexpr bool PIPE = R == 16;
     const int cs = c < MZH_A ? c : MZH_A - 1;
+    uint3 sv;   // N | X, R, P of this lane's slot: one dwordx3
+    double Wl;  // W of this lane's slot
+    auto issue = [&](int en, int ecur) {
+      const MzhBlock* b = tb + (en >= 0 ? en : ecur);
+      sv = *reinterpret_cast<const uint3*>(&b->sl[cs]);
+      Wl = b->W[cs];
+    };
+    if (PIPE) issue(nx >> 16, 0);
+    // the picking lane records the path entry and its own statistics
+    if (c == pick) {
+      path[r * PL] = (uint16_t)pick;
+      st.pc[r][0] = MzhPathEnt{Wc, Rc, Nc};
+    }
 #ifdef MZH_STAMPS
     asm volatile("" ::"v"(nx), "v"(pf0));
 #endif
@@ -255,12 +267,11 @@ struct MzhTree {
     while ((nx >> 16) >= 0) {
       e = nx >> 16;
       const int Np = nx & 0xFFFF;
-      const MzhBlock* b = tb + e;
-      const uint3 sv = *reinterpret_cast<const uint3*>(&b->sl[cs]);  // N | X, R, P: one dwordx3
+      if (!PIPE) issue(e, e);
       const double tnp = table[Np];  // LDS: in flight beside the block loads
       int nxc = (int)sv.x;
       Rc = __uint_as_float(sv.y);
-      Wc = b->W[cs];
+      Wc = Wl;
       const float Pc = __uint_as_float(sv.z);
       if (c >= MZH_A) nxc = (int)0xFFFF0000;
 #ifdef MZH_STAMPS
@@ -286,11 +297,13 @@ struct MzhTree {
       asm volatile("" ::"v"(pick));
 #endif
       MZH_LSTAMP(2);
+      const int nxn = mzh_group_take(nxc, c == pick);
+      if (PIPE) issue(nxn >> 16, e);
       if (c == pick) {
         path[r * PL + depth] = (uint16_t)(e * 8 + pick);
         if (depth < DC) st.pc[r][depth] = MzhPathEnt{Wc, Rc, Nc};
       }
-      nx = mzh_group_take(nxc, c == pick);
+      nx = nxn;
       depth++;
 #ifdef MZH_STAMPS
       asm volatile("" ::"v"(nx));
