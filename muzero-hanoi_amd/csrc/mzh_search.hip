@@ -238,7 +238,7 @@ static hipError_t launch_search_m(const MzhNet& net, const MzhSearchParams& p, h
 template <int R, bool REPLAY, bool OHL, bool SUP33>
 static hipError_t launch_search_s(const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
   // caller-given bounds: the instantiation that checks for a subnormal max - min (never with OHL: the
-  // one-hot table is only an LDS placement choice of the 32-root tile)
+  // one-hot table is only an LDS placement choice)
   if constexpr (!OHL) {
     if (p.minmax_in) return launch_search_m<R, REPLAY, OHL, SUP33, true>(net, p, stream);
   }
@@ -262,7 +262,9 @@ hipError_t mzh_launch_search(int R, bool replay, const MzhNet& net, const MzhSea
     if (search_smem_bytes<32>(p.S, true) <= kLdsBytes && !p.minmax_in) return launch_search_t<32, false, true>(net, p, stream);
     return launch_search_t<32, false, false>(net, p, stream);
   }
-  return replay ? launch_search_t<16, true, false>(net, p, stream) : launch_search_t<16, false, false>(net, p, stream);
+  if (replay) return launch_search_t<16, true, false>(net, p, stream);
+  if (search_smem_bytes<16>(p.S, true) <= kLdsBytes && !p.minmax_in) return launch_search_t<16, false, true>(net, p, stream);
+  return launch_search_t<16, false, false>(net, p, stream);
 }
 
 template <int R>
