@@ -76,9 +76,10 @@ __device__ unsigned long long mzh_stamp_acc[8][MZH_NSTAMP];
 // ------------------------------------------------------------------------------------------
 // fp32 math (networks.py:152-196)
 // ------------------------------------------------------------------------------------------
+// Branch-free: the polynomial runs for every lane and the range checks select the result (a
+// divergent branch per exponential costs an exec-mask round trip; outside the range the computed
+// value is discarded), so the result is the same as testing first
 __device__ __forceinline__ float mzh_expf(float x) {
-  if (x < -87.0f) return 0.0f;
-  if (x > 88.0f) return __builtin_inff();
   float n = __builtin_rintf(x * 1.44269502162933349609375f);
   float r = __builtin_fmaf(n, -0.693359375f, x);
   r = __builtin_fmaf(n, 2.12194440e-4f, r);
@@ -92,12 +93,12 @@ __device__ __forceinline__ float mzh_expf(float x) {
   p = __builtin_fmaf(p, r2, r);
   p = p + 1.0f;
   int ni = (int)n;
-  return p * __int_as_float((ni + 127) << 23);
+  const float e = p * __int_as_float((ni + 127) << 23);
+  return x < -87.0f ? 0.0f : (x > 88.0f ? __builtin_inff() : e);
 }
 
-// mzh_expf for x <= 0 (softmax arguments l - max): the overflow branch dropped
+// mzh_expf for x <= 0 (softmax arguments l - max): the overflow check dropped
 __device__ __forceinline__ float mzh_expf_np(float x) {
-  if (x < -87.0f) return 0.0f;
   float n = __builtin_rintf(x * 1.44269502162933349609375f);
   float r = __builtin_fmaf(n, -0.693359375f, x);
   r = __builtin_fmaf(n, 2.12194440e-4f, r);
@@ -111,7 +112,8 @@ __device__ __forceinline__ float mzh_expf_np(float x) {
   p = __builtin_fmaf(p, r2, r);
   p = p + 1.0f;
   int ni = (int)n;
-  return p * __int_as_float((ni + 127) << 23);
+  const float e = p * __int_as_float((ni + 127) << 23);
+  return x < -87.0f ? 0.0f : e;
 }
 
 // _signed_parabolic (networks.py:186-189)

@@ -234,8 +234,8 @@ __device__ __forceinline__ float mzw_head(const floatx4 (&l)[NO][NT], int n, int
   m = mzw_max4g(m);
   float e[9];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) e[s] = mzh_expf(L[s] - m);
-  e[8] = v8 ? mzh_expf(L[8] - m) : 0.0f;
+  for (int s = 0; s < 8; ++s) e[s] = mzh_expf_np(L[s] - m);  // arguments <= 0
+  e[8] = v8 ? mzh_expf_np(L[8] - m) : 0.0f;
   float s0 = e[0];
   s0 = s0 + e[2];
   s0 = s0 + e[4];
@@ -291,8 +291,9 @@ __device__ __forceinline__ floatx4 mzw_policy(const floatx4 l, int lane) {
     m = l[3] > m ? l[3] : m;
   }
   m = mzw_max4g(m);
-  const float e0 = ok01 ? mzh_expf(l[0] - m) : 0.0f, e1 = ok01 ? mzh_expf(l[1] - m) : 0.0f;
-  const float e2 = ok23 ? mzh_expf(l[2] - m) : 0.0f, e3 = ok23 ? mzh_expf(l[3] - m) : 0.0f;
+  // arguments <= 0 on the lanes whose result is used
+  const float e0 = ok01 ? mzh_expf_np(l[0] - m) : 0.0f, e1 = ok01 ? mzh_expf_np(l[1] - m) : 0.0f;
+  const float e2 = ok23 ? mzh_expf_np(l[2] - m) : 0.0f, e3 = ok23 ? mzh_expf_np(l[3] - m) : 0.0f;
   float t = (e0 + e1) + (e2 + e3);
   t = mzw_add16(t);  // group 0: ((s0+s1)+(s2+s3)) + ((s4+s5)+(0+0))
   const float y = 1.0f / t;
