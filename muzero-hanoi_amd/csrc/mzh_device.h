@@ -693,14 +693,16 @@ __device__ __forceinline__ MzhHeadOut mzh_heads_row(SM& sm, int row, int q, int 
   for (int h = 0; h < 2; ++h) m[h] = mzh_max8(m[h]);
   // every exponent argument is <= 0; xmin tracks the smallest one that feeds a probability
   const float xp = lg - mp;
-  const float ep = q < MZH_A ? mzh_expf_np(xp) : 0.0f;
+  const float epx = mzh_expf_np(xp);  // every lane (no divergent branch); lanes 6, 7 discard it
+  const float ep = q < MZH_A ? epx : 0.0f;
   float xmin = q < MZH_A ? xp : 0.0f;
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
       const float xv = e[h][i] - m[h];
-      e[h][i] = (q + 8 * i < 33) ? mzh_expf_np(xv) : 0.0f;
+      const float ex = mzh_expf_np(xv);  // every lane (no divergent branch)
+      e[h][i] = (q + 8 * i < 33) ? ex : 0.0f;
       if (h < nh && q + 8 * i < 33) xmin = xv < xmin ? xv : xmin;
     }
   float sh[2];

@@ -435,7 +435,7 @@ struct MzhTree {
         const double rw = (jp == depth - 1) ? (double)rew : (double)pe.R;
         const double W = pe.W + bv[k];
         const int N = pe.N + 1;
-        if (e == 0) {
+        if (jp == 0) {  // the root's child (path entry 0 is the only one with e = 0)
           rb.W[a] = W;
           rb.N[a] = N;
         } else {

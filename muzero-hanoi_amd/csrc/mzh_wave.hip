@@ -235,7 +235,8 @@ __device__ __forceinline__ float mzw_head(const floatx4 (&l)[NO][NT], int n, int
   float e[9];
 #pragma unroll
   for (int s = 0; s < 8; ++s) e[s] = mzh_expf_np(L[s] - m);  // arguments <= 0
-  e[8] = v8 ? mzh_expf_np(L[8] - m) : 0.0f;
+  e[8] = mzh_expf_np(L[8] - m);  // evaluated on every lane (no divergent branch), kept on group 0
+  e[8] = v8 ? e[8] : 0.0f;
   float s0 = e[0];
   s0 = s0 + e[2];
   s0 = s0 + e[4];
@@ -291,9 +292,11 @@ __device__ __forceinline__ floatx4 mzw_policy(const floatx4 l, int lane) {
     m = l[3] > m ? l[3] : m;
   }
   m = mzw_max4g(m);
-  // arguments <= 0 on the lanes whose result is used
-  const float e0 = ok01 ? mzh_expf_np(l[0] - m) : 0.0f, e1 = ok01 ? mzh_expf_np(l[1] - m) : 0.0f;
-  const float e2 = ok23 ? mzh_expf_np(l[2] - m) : 0.0f, e3 = ok23 ? mzh_expf_np(l[3] - m) : 0.0f;
+  // arguments <= 0 on the lanes whose result is used; evaluated on every lane (no divergent branch)
+  const float x0 = mzh_expf_np(l[0] - m), x1 = mzh_expf_np(l[1] - m);
+  const float x2 = mzh_expf_np(l[2] - m), x3 = mzh_expf_np(l[3] - m);
+  const float e0 = ok01 ? x0 : 0.0f, e1 = ok01 ? x1 : 0.0f;
+  const float e2 = ok23 ? x2 : 0.0f, e3 = ok23 ? x3 : 0.0f;
   float t = (e0 + e1) + (e2 + e3);
   t = mzw_add16(t);  // group 0: ((s0+s1)+(s2+s3)) + ((s4+s5)+(0+0))
   const float y = 1.0f / t;
@@ -771,49 +774,65 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
       double lmax = -__builtin_inf(), lmin = __builtin_inf();
       // path entry j: slot (parent expanded index * 8 + child) and the child's statistics at
       // selection time; entry j - 1 is loaded while entry j is processed
-      auto load_entry = [&](int j, int& slot, double& W, float& R, int& N) {
-        if (j < MZW_DC) {
-          slot = ws.path[j][rho];
-          W = ws.pcW[j][rho];
-          R = ws.pcR[j][rho];
-          N = ws.pcN[j][rho];
-        } else {
-          slot = p.pathx[(size_t)rroot * E + j];
-          const int e = slot >> 3, a = slot & 7;
-          W = tb[e].W[a];
-          R = tb[e].R[a];
-          N = tb[e].nx[a].N;
-        }
+      auto load_lds = [&](int j, int& slot, double& W, float& R, int& N) {
+        slot = ws.path[j][rho];
+        W = ws.pcW[j][rho];
+        R = ws.pcR[j][rho];
+        N = ws.pcN[j][rho];
+      };
+      auto load_hbm = [&](int j, int& slot, double& W, float& R, int& N) {  // depths >= MZW_DC
+        slot = p.pathx[(size_t)rroot * E + j];
+        const int e = slot >> 3, a = slot & 7;
+        W = tb[e].W[a];
+        R = tb[e].R[a];
+        N = tb[e].nx[a].N;
       };
       int slot;
       double Wj;
       float Rj;
       int Nj;
-      load_entry(depth - 1, slot, Wj, Rj, Nj);
-      for (int j = depth - 1; j >= 0; --j) {
-        int slot_n = 0, Nj_n = 0;
-        double Wj_n = 0.0;
-        float Rj_n = 0.0f;
-        if (j > 0) load_entry(j - 1, slot_n, Wj_n, Rj_n, Nj_n);
-        const int e = slot >> 3, a = slot & 7;
+      // path node j: its statistics (W += v, N += 1), the MinMaxStats candidate, the value chain
+      auto node = [&](int j, double& Wn, int& Nn) {
         const double rw = (j == depth - 1) ? (double)rr : (double)Rj;
-        const double Wn = Wj + v;
-        const int Nn = Nj + 1;
+        Wn = Wj + v;
+        Nn = Nj + 1;
         const double q = rw + disc * mzw_div(Wn, (double)Nn, inv[Nn]);  // MinMaxStats input
-        if (e == 0) {
-          ws.rW[a][rho] = Wn;
-          ws.rN[a][rho] = Nn;
-        } else {
-          tb[e].W[a] = Wn;
-          tb[e].nx[a].N = (uint16_t)Nn;
-        }
         lmax = q > lmax ? q : lmax;
         lmin = q < lmin ? q : lmin;
         v = rw + disc * v;
+      };
+      if (depth - 1 < MZW_DC) load_lds(depth - 1, slot, Wj, Rj, Nj);
+      else load_hbm(depth - 1, slot, Wj, Rj, Nj);
+      // depths j >= 1 sit in HBM tree blocks (e >= 1), depth 0 is the root's child in LDS (peeled: no
+      // per-node branch on where the statistics live); entry j - 1 loaded while node j is processed
+      int j = depth - 1;
+      auto hbm_node = [&](int jn) {
+        const int e = slot >> 3, a = slot & 7;
+        double Wn;
+        int Nn;
+        node(jn, Wn, Nn);
+        tb[e].W[a] = Wn;
+        tb[e].nx[a].N = (uint16_t)Nn;
+      };
+      for (; j >= 1; --j) {
+        int slot_n, Nj_n;
+        double Wj_n;
+        float Rj_n;
+        if (j - 1 < MZW_DC) load_lds(j - 1, slot_n, Wj_n, Rj_n, Nj_n);
+        else load_hbm(j - 1, slot_n, Wj_n, Rj_n, Nj_n);  // paths deeper than the LDS cache (rare)
+        hbm_node(j);
         slot = slot_n;
         Wj = Wj_n;
         Rj = Rj_n;
         Nj = Nj_n;
+      }
+      {  // depth 0: the root's child (path slot = child index, e = 0)
+        const int a = slot & 7;
+        double Wn;
+        int Nn;
+        node(0, Wn, Nn);
+        ws.rW[a][rho] = Wn;
+        ws.rN[a][rho] = Nn;
       }
       rootW = rootW + v;
       rootN = rootN + 1;
