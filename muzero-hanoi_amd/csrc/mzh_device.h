@@ -462,10 +462,17 @@ __device__ __forceinline__ void mzh_fetch(floatx4* f, float* bv, const MzhChunk&
 // that stalls every wave on the CU's address unit.
 // The last k-block runs tile-major, each tile's epilogue right behind its last MFMA, so the
 // stores of tile q overlap the MFMAs of tiles q+1.. instead of trailing the chain.
-template <int MT, int NJ, int KB, bool ALL = false, int PT = 0, int PNB = 0, bool NAT = false>
+struct MzhNoMid {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+// MID (optional): independent VALU / LDS work, mid(kb) placed in the region of k-block kb's MFMAs, so
+// it issues under their execution instead of on the phase's critical path (the latent normalisation
+// beside rwd0; it must neither read this chain's output nor write its A operand or its LDS output)
+template <int MT, int NJ, int KB, bool ALL = false, int PT = 0, int PNB = 0, bool NAT = false, class MID = MzhNoMid>
 __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhChunk& c, const float* A, int lda,
                                               bool relu, const float* oht, const int* act, int lane,
-                                              const MzhChunk* pc = nullptr, const floatx4* areg = nullptr) {
+                                              const MzhChunk* pc = nullptr, const floatx4* areg = nullptr,
+                                              MID mid = MID{}) {
   // areg (optional): the A operand of all KB k-blocks already in registers, [kb * MT + m] (chunks
   // of one phase that share A load it once)
   static_assert(PT <= 16 && PNB <= 4, "ring chunk too large");
@@ -492,18 +499,27 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
     for (int m = 0; m < MT; ++m) a[0][m] = *reinterpret_cast<const floatx4*>(arow + m * 16 * lda);
   }
   auto aop = [&](int kb, int m) -> const floatx4& { return areg ? areg[kb * MT + m] : a[kb & 1][m]; };
+  // the one-hot columns: the row actions are read here, the column values (only the epilogue adds
+  // them) in k-block 1's region, under the MFMAs of k-block 0
   float oh[NJ * MT * 4];
+  int acts[MT * 4];
   if (oht) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
+      for (int i = 0; i < 4; ++i) acts[m * 4 + i] = act[m * 16 + g * 4 + i];
+  }
+  auto gather_oh = [&]() {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float* ohrow = oht + act[m * 16 + g * 4 + i] * MZH_F + r;
+        const float* ohrow = oht + acts[m * 4 + i] * MZH_F + r;
 #pragma unroll
         for (int q = 0; q < NJ; ++q) oh[(q * MT + m) * 4 + i] = ohrow[c.col0[q]];
       }
-  }
+  };
   auto epilogue = [&](int q) {
     // output column col0 + r; a hidden / latent unit is stored at its k-block-order position
     const int pos = c.col0[q] + (NAT ? r : 4 * (r & 3) + (r >> 2));
@@ -530,6 +546,8 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
         a[(kb + 1) & 1][m] = *reinterpret_cast<const floatx4*>(arow + m * 16 * lda + (kb + 1) * 16);
     }
     __builtin_amdgcn_sched_barrier(0);
+    if (oht && kb == (KB > 1 ? 1 : 0)) gather_oh();
+    mid(kb);
     if (kb + 1 < KB) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -577,75 +595,89 @@ __device__ __forceinline__ float mzh_fdiv(float a, float b, float y, bool& slow)
   return res;
 }
 
+// One pass over the rows in three steps -- load (LDS read), reduce (row min / max), finish (the
+// quotients, LDS store) -- so a caller can spread it over an MFMA chain.  finish<false>: the Markstein
+// quotients; returns whether some lane of the wave flagged `slow` (wave-uniform), in which case the
+// caller reruns the pass with finish<true> (IEEE division, the same results wherever the Markstein
+// form is exact).  src is left untouched, so the rerun may come later.
+//   R == 16: 16 rows over all 256 threads -- 16 lanes per row (one DPP row), 4 elements per lane, so
+//   all four waves share the work (8 lanes per row leave waves 2, 3 idle at the next barrier); with
+//   the dynamics one-hot columns in LDS for 16-root tiles too: 4,096 roots 0.921 -> 0.910 ms.
+//   Otherwise 8 lanes per row, 8 elements per lane, R / 32 rows per thread.
+template <int R>
+struct MzhNormPass {
+  static constexpr int NE = R == 16 ? 4 : 8, NR = R == 16 ? 1 : R / 32;
+  static_assert(R == 16 || R % 32 == 0, "normalisation rows");
+  float v[NR][NE];
+  float mn[NR];
+  __device__ __forceinline__ int off(int tid, int k) const {
+    return R == 16 ? (tid >> 4) * MZH_LD64 + (tid & 15) * 4 : (k * 32 + (tid >> 3)) * MZH_LD64 + (tid & 7) * 8;
+  }
+  __device__ __forceinline__ void load(const float* src, int tid) {
+#pragma unroll
+    for (int k = 0; k < NR; ++k)
+#pragma unroll
+      for (int h = 0; h < NE; h += 4) {
+        const floatx4 t = *reinterpret_cast<const floatx4*>(src + off(tid, k) + h);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[k][h + i] = t[i];
+      }
+  }
+  float d[NR];
+  __device__ __forceinline__ void reduce() {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      float lo = v[k][0], hi = v[k][0];
+#pragma unroll
+      for (int i = 1; i < NE; ++i) {
+        lo = v[k][i] < lo ? v[k][i] : lo;
+        hi = v[k][i] > hi ? v[k][i] : hi;
+      }
+      lo = mzh_min8(lo);
+      hi = mzh_max8(hi);
+      if (R == 16) {  // the two 8-lane halves of the row (row_ror:8)
+        const float tn = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(lo), 0x128, 0xF, 0xF, true));
+        const float tx = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(hi), 0x128, 0xF, 0xF, true));
+        lo = tn < lo ? tn : lo;
+        hi = tx > hi ? tx : hi;
+      }
+      mn[k] = lo;
+      d[k] = (hi - lo) + 9.999999939225290290778502821922302246094e-09f;
+    }
+  }
+  template <bool EXACT>
+  __device__ __forceinline__ bool finish(float* dst, int tid) const {
+    bool slow = false;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      float o[NE];
+      if (EXACT) {
+#pragma unroll
+        for (int i = 0; i < NE; ++i) o[i] = (v[k][i] - mn[k]) / d[k];
+      } else {
+        const float y = 1.0f / d[k];
+#pragma unroll
+        for (int i = 0; i < NE; ++i) o[i] = mzh_fdiv(v[k][i] - mn[k], d[k], y, slow);
+      }
+#pragma unroll
+      for (int h = 0; h < NE; h += 4)
+        *reinterpret_cast<floatx4*>(dst + off(tid, k) + h) = floatx4{o[h], o[h + 1], o[h + 2], o[h + 3]};
+    }
+    return !EXACT && __ballot(slow) != 0;
+  }
+};
+
+template <int R, bool EXACT>
+__device__ __forceinline__ bool mzh_normalize_rows(const float* src, float* dst, int tid) {
+  MzhNormPass<R> n;
+  n.load(src, tid);
+  n.reduce();
+  return n.template finish<EXACT>(dst, tid);
+}
+
 template <int R>
 __device__ __forceinline__ void mzh_normalize_par(const float* src, float* dst, int tid) {
-  if constexpr (R == 16) {
-    // 16 rows over all 256 threads: 16 lanes per row (one DPP row), 4 elements per lane, so all four
-    // waves share the work (8 lanes per row leave waves 2, 3 idle at the next barrier); with the
-    // dynamics one-hot columns in LDS for 16-root tiles too: 4,096 roots 0.921 -> 0.910 ms
-    const int row = tid >> 4, part = tid & 15;
-    const floatx4 v = *reinterpret_cast<const floatx4*>(src + row * MZH_LD64 + part * 4);
-    float mn = v[0], mx = v[0];
-#pragma unroll
-    for (int i = 1; i < 4; ++i) {
-      mn = v[i] < mn ? v[i] : mn;
-      mx = v[i] > mx ? v[i] : mx;
-    }
-    mn = mzh_min8(mn);
-    mx = mzh_max8(mx);
-    {  // the two 8-lane halves of the row (row_ror:8)
-      const float tn = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(mn), 0x128, 0xF, 0xF, true));
-      const float tx = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(mx), 0x128, 0xF, 0xF, true));
-      mn = tn < mn ? tn : mn;
-      mx = tx > mx ? tx : mx;
-    }
-    const float d = (mx - mn) + 9.999999939225290290778502821922302246094e-09f;
-    floatx4 w;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = v[i] - mn;
-    const float y = 1.0f / d;
-    bool slow = false;
-    floatx4 o;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = mzh_fdiv(w[i], d, y, slow);
-    if (__builtin_expect(__ballot(slow) != 0, 0)) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) o[i] = w[i] / d;
-    }
-    *reinterpret_cast<floatx4*>(dst + row * MZH_LD64 + part * 4) = o;
-    return;
-  }
-#pragma unroll
-  for (int base = 0; base < R; base += MZH_THREADS / 8) {
-    const int row = base + (tid >> 3), part = tid & 7;
-    if (row < R) {
-      float v[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = src[row * MZH_LD64 + part * 8 + i];
-      float mn = v[0], mx = v[0];
-#pragma unroll
-      for (int i = 1; i < 8; ++i) {
-        mn = v[i] < mn ? v[i] : mn;
-        mx = v[i] > mx ? v[i] : mx;
-      }
-      mn = mzh_min8(mn);
-      mx = mzh_max8(mx);
-      const float d = (mx - mn) + 9.999999939225290290778502821922302246094e-09f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = v[i] - mn;
-      const float y = 1.0f / d;
-      bool slow = false;
-      float o[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = mzh_fdiv(v[i], d, y, slow);
-      if (__builtin_expect(__ballot(slow) != 0, 0)) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = v[i] / d;
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) dst[row * MZH_LD64 + part * 8 + i] = o[i];
-    }
-  }
+  if (__builtin_expect(mzh_normalize_rows<R, false>(src, dst, tid), 0)) mzh_normalize_rows<R, true>(src, dst, tid);
 }
 
 // Heads (networks.py:83,109,152-189): 8 lanes per row; the value and reward heads of a row run
@@ -903,10 +935,18 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
   MZH_STAMP(3);
   bar();
   MZH_STAMP(4);
-  mzh_normalize_par<R>(sm.hraw, sm.x, tid);
   MZH_STAMP(5);
-  mzh_mma_store<MT, 4, 4, true, 16, 4>(fa, ba, c_rwd0, sm.hraw, MZH_LD64, true, nullptr, nullptr, lane,
-                                       &c_p2);  // rwd0 on h' (networks.py:132)
+  // rwd0 on h' (networks.py:132); the normalisation only reads h' too (writing sm.x, read after the
+  // next barrier): its pass issues under rwd0's MFMAs, the rare exact rerun after them
+  MzhNormPass<R> norm;
+  bool slow = false;
+  mzh_mma_store<MT, 4, 4, true, 16, 4>(fa, ba, c_rwd0, sm.hraw, MZH_LD64, true, nullptr, nullptr, lane, &c_p2,
+                                       nullptr, [&](int kb) {
+                                         if (kb == 0) norm.load(sm.hraw, tid);
+                                         if (kb == 1) norm.reduce();
+                                         if (kb == 2) slow = norm.template finish<false>(sm.x, tid);
+                                       });
+  if (__builtin_expect(slow, 0)) norm.template finish<true>(sm.x, tid);
   MZH_STAMP(6);
   bar();
   MZH_STAMP(7);
