@@ -167,11 +167,8 @@ __device__ __forceinline__ float kcomb(const float* P, int ldp, int r, int c) {
   return v;
 }
 
-// threads of a row-kernel workgroup (256: one wave per SIMD; 512: two)
-#ifndef MZT_RNT
-#define MZT_RNT 512
-#endif
-constexpr int RNT = MZT_RNT;
+// threads of a row-kernel workgroup: 512, two waves per SIMD (measured against 256, one per SIMD)
+constexpr int RNT = 512;
 
 // LDS plan of the rows kernel (floats), U steps, R rows
 constexpr int RED_PER_ROW = 12 * RNT;  // split-K partials: 3 areas x (RNT / 64 chunks x 256 outputs)
@@ -564,10 +561,7 @@ __device__ __forceinline__ void adam(float* pp, float* mm, float* vv, size_t i, 
   vv[i] = v;
 }
 
-#ifndef MZT_NW2
-#define MZT_NW2 16
-#endif
-constexpr int NW2 = MZT_NW2;  // waves per weight tile: they split the B*U rows
+constexpr int NW2 = 16;  // waves per weight tile: they split the B*U rows
 __global__ __launch_bounds__(64 * NW2) void mzt_grad_adam_kernel(MztGradParams P) {
   constexpr int NP = 4 * NW2;  // bias row classes (16 columns x NP)
   __shared__ float red[NW2][16][17];
