@@ -116,6 +116,27 @@ __device__ __forceinline__ float mzh_expf_np(float x) {
   return x < -87.0f ? 0.0f : e;
 }
 
+// _signed_parabolic of two independent values as one packed chain (v_pk_* ops; the same
+// operations per element as mzh_signed_parabolic below, so the same results)
+typedef float mzh_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ mzh_f2 mzh_signed_parabolic2(mzh_f2 x) {
+  const mzh_f2 a = {__builtin_fabsf(x.x), __builtin_fabsf(x.y)};
+  mzh_f2 t = 1.00100004673004150390625f + a;
+  t = 0.0040000001899898052215576171875f * t;
+  t = 1.0f + t;
+  t = mzh_f2{__builtin_sqrtf(t.x), __builtin_sqrtf(t.y)};
+  t = t * 0.5f;  // t / 2.0f: exact
+  {
+    const mzh_f2 b = 0.001000000047497451305389404296875f, y = 0x1.f3fffep+9f;
+    const mzh_f2 q = t * y;
+    const mzh_f2 r = __builtin_elementwise_fma(-q, b, t);
+    t = __builtin_elementwise_fma(r, y, q);
+  }
+  const mzh_f2 z = t - 500.0f;
+  const mzh_f2 sg = {x.x > 0.0f ? 1.0f : (x.x < 0.0f ? -1.0f : 0.0f), x.y > 0.0f ? 1.0f : (x.y < 0.0f ? -1.0f : 0.0f)};
+  return sg * (z * z - 1.0f);
+}
+
 // _signed_parabolic (networks.py:186-189)
 __device__ __forceinline__ float mzh_signed_parabolic(float x) {
   float a = __builtin_fabsf(x);
@@ -793,8 +814,9 @@ __device__ __forceinline__ MzhHeadOut mzh_heads_row(SM& sm, int row, int q, int 
 #pragma unroll
   for (int h = 0; h < 2; ++h) x[h] = mzh_sum8(x[h]);
   if (nh > 0) {
-    out.value = mzh_signed_parabolic(x[0]);
-    out.reward = nh > 1 ? mzh_signed_parabolic(x[1]) : 0.0f;
+    const mzh_f2 vr = mzh_signed_parabolic2(mzh_f2{x[0], x[1]});  // value and reward side by side
+    out.value = vr.x;
+    out.reward = nh > 1 ? vr.y : 0.0f;
     if (STORE && q == 0) {
       sm.value[row] = out.value;
       sm.reward[row] = out.reward;

@@ -53,7 +53,7 @@ template <int R, int DC_>
 struct SearchSmem {
   static constexpr int DC = DC_;
   MzhRootBlk root[R];
-  MzhPathEnt pc[R][DC];
+  MzhPathEnt pc[R][DC + 1];  // entry DC: where the selection's stores of deeper levels land (never read)
   double rootW[R];
   double mm[R][4];  // MinMaxStats (maximum, minimum) + normaliser (max - min, RN(1/(max - min)))
   int rootN[R];
@@ -299,9 +299,9 @@ struct MzhTree {
       MZH_LSTAMP(2);
       const int nxn = mzh_group_take(nxc, c == pick);
       if (PIPE) issue(nxn >> 16, e);
-      if (c == pick) {
+      if (c == pick) {  // two stores, no nested branch (levels past the cache land in entry DC)
         path[r * PL + depth] = (uint16_t)(e * 8 + pick);
-        if (depth < DC) st.pc[r][depth] = MzhPathEnt{Wc, Rc, Nc};
+        st.pc[r][depth < DC ? depth : DC] = MzhPathEnt{Wc, Rc, Nc};
       }
       nx = nxn;
       depth++;
