@@ -200,6 +200,53 @@ def test_search_confident_heads_vs_oracle(mzh, oracle, kernel):
         assert np.array_equal(o[k], ref[rk]), k
 
 
+def _tiny_latent_gap(oracle):
+    """weights_N4_s0 with the dynamics output layer made constant: h' = its bias, one unit 2^-110
+    above the row minimum.  That unit's Markstein quotient in the latent normalisation flags `slow`
+    (a numerator below 2^-100), so every kernel takes its exact-division rerun -- in the
+    cooperative kernels the pass that runs after rwd0's MFMA chain (mzh_mlp_recurrent_body)"""
+    w, in_dim, sup = oracle.load_weights_npz(f"{GOLDEN}/weights_N4_s0.npz")
+    w = {k: v.copy() for k, v in w.items()}
+    w["dynamic_net.2.weight"][:] = 0.0
+    b = np.random.RandomState(11).uniform(0.25, 1.0, 64).astype(np.float32)
+    b[3], b[17] = 0.0, np.float32(2.0 ** -110)
+    w["dynamic_net.2.bias"][:] = b
+    return oracle.flat_weights(w), in_dim, sup
+
+
+def test_normalisation_exact_rerun_vs_oracle(mzh, oracle):
+    """recurrent_inference with a latent unit 2^-110 above the row minimum == the oracle bit for bit"""
+    flat, in_dim, sup = _tiny_latent_gap(oracle)
+    B = 300
+    rs = np.random.RandomState(6)
+    h = rs.uniform(0, 1, (B, 64)).astype(np.float32)
+    a = rs.randint(0, 6, B).astype(np.int32)
+    orr = oracle.recurrent_inference(flat, in_dim, sup, h, a)
+    assert (orr["h"] > 0).any() and (orr["h"][orr["h"] > 0] < 2.0 ** -100).any()  # the tiny quotient
+    eng = _engine(mzh, 4, 4, B, 33, flat)
+    ri = eng.recurrent_inference(torch.tensor(h, device=DEV), torch.tensor(a, device=DEV))
+    for k in ("h", "pi", "value", "reward"):
+        assert np.array_equal(ri[k].cpu().numpy(), orr[k]), k
+
+
+@pytest.mark.parametrize("kernel,tile", [("coop", 16), ("coop", 32), ("wave", None), ("wave16", None)])
+def test_search_normalisation_exact_rerun_vs_oracle(mzh, oracle, kernel, tile):
+    """the fused searches with every expansion's latent normalised by the exact-division rerun ==
+    the oracle's, every output bit for bit (both cooperative tiles and the wave kernels)"""
+    flat, in_dim, sup = _tiny_latent_gap(oracle)
+    B, S, n = 100, 12, 4
+    obs, noise, tie, u = _random_search_inputs(B, n, 78)
+    eng = _engine(mzh, n, S, B, sup, flat)
+    tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
+    o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0, kernel=kernel,
+                   tile=tile)
+    o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+    ref = oracle.search(n, S, obs, flat=flat, support=sup, noise=noise, tie_idx=tie, action_u=u, temperature=1.0)
+    for k, rk in (("visits", "visits"), ("root_q", "rootQ"), ("action", "action"), ("sel_steps", "sel_steps"),
+                  ("extra_ties", "extra_ties")):
+        assert np.array_equal(o[k], ref[rk]), k
+
+
 def _run_replay_case(mzh, g, kernel=None):
     S, n = int(g["s"]), int(g["n"])
     det, T = bool(g["deterministic"]), float(g["temperature"])
