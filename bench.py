@@ -74,11 +74,16 @@ def parse():
                    help="BASELINE.json configs[K]; the global batch is sharded over the ranks (strong scaling)")
     p.add_argument("--roots-per-gpu", type=int, default=None,
                    help="weak scaling: this many roots on every GPU (overrides the config's global batch)")
+    p.add_argument("--shard", default=None, metavar="R/W",
+                   help="run rank R's shard of the config's global batch for a W-GPU job, alone on this GPU "
+                        "(the per-GPU work of the W-GPU bench, same roots and draws; value = this GPU's sims/s)")
     p.add_argument("--sims", type=int, default=None)
     p.add_argument("--disks", type=int, default=None)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-gather", action="store_true")
     p.add_argument("--no-tree", action="store_true", help="skip the live select/backup (replay) measurement")
+    p.add_argument("--no-minmax-leg", action="store_true",
+                   help="skip timing the instantiation searches with caller MinMaxStats bounds run (training / acting)")
     p.add_argument("--kernel", choices=["auto", "coop", "wave", "wave16"], default="auto")
     p.add_argument("--tile", type=int, choices=[16, 32], default=None,
                    help="cooperative kernel: roots per workgroup (default by batch size)")
@@ -240,10 +245,21 @@ def tree_bytes(sel_steps_sum, n_roots, S, expand_bytes):
     return SEL_BYTES * sel_steps_sum + BACKUP_BYTES * (sel_steps_sum + n_roots * S) + expand_bytes * n_roots * S
 
 
-def traffic_key(n_disks, S, B, kern="auto"):
+def search_plan(S, B, kern="auto", tile=None, replay=False, minmax_in=False, support=33):
+    """the launch plan libmzh reports for this workload (mzh_search_plan_query: the same host code
+    that picks the instantiation mzh_search launches -- kernel, tile, template arguments)"""
+    from muzero_hanoi_amd import _lib, engine
+
+    return _lib.search_plan(support, B, S, engine.search_flags(None if kern == "auto" else kern, tile),
+                            replay=replay, minmax_in=minmax_in)
+
+
+def traffic_key(n_disks, S, B, kern="auto", tile=None, minmax_in=False):
     """the key of one bench workload in profiles/traffic_latest.json (tools/traffic.py writes it
-    from the same function): disks, sims, roots on this GPU and the kernel that serves them"""
-    return f"hanoi{n_disks}_s{S}_roots{B}_{kernel_name(kern, B)[0]}"
+    from the same function): disks, sims, roots on this GPU and the fused kernel instantiation the
+    library launches for them"""
+    k = search_plan(S, B, kern, tile, minmax_in=minmax_in)["kernel"].replace(" ", "")
+    return f"hanoi{n_disks}_s{S}_roots{B}_{k}"
 
 
 def workload_shape(config, world=1, rank=0, roots_per_gpu=None, disks=None, sims=None):
@@ -276,12 +292,13 @@ def lookup_traffic(path, key):
     return ent, "rocprofv3 PMC of this build (tools/prof.sh + tools/traffic.py)"
 
 
-def kernel_name(kern, B):
-    """the search kernel mzh_api.hip choose_kernel() / pick_tile() launches for B roots"""
-    kern_sel = kern if kern != "auto" else ("wave" if B >= 53248 else "wave16" if B > 8192 else "coop")
-    coop_rows = 32 if B > 4096 else 16
-    return kern_sel, {"wave": "mzh_wave_kernel<2,{r},true>", "wave16": "mzh_wave_kernel<1,{r},true>",
-                      "coop": f"mzh_search_kernel<{coop_rows},{{r}},*,true>"}[kern_sel]
+def waves_per_simd(plan, B):
+    """waves sharing a SIMD: the wave kernel runs B / roots_per_wave waves, two 4-wave workgroups per
+    CU at most (1,024 SIMDs); the cooperative kernel one 4-wave workgroup per CU"""
+    if not plan["wave"]:
+        return 1
+    waves = -(-B // plan["roots_per_wave"])
+    return min(2, max(1, -(-waves // 1024)))
 
 
 def main():
@@ -297,6 +314,10 @@ def main():
     weak = a.roots_per_gpu is not None
     if weak:
         GB = world * a.roots_per_gpu
+    # --shard R/W: this process plays rank R of a W-GPU job (one GPU, no collective)
+    srank, sworld = (rank, world) if a.shard is None else map(int, a.shard.split("/"))
+    if a.shard is not None and (world > 1 or weak or not 0 <= srank < sworld):
+        raise SystemExit("--shard R/W needs one process, no --roots-per-gpu, and 0 <= R < W")
 
     # CPU baseline first (rank 0, N=1): spawned host processes, before this process touches the GPU
     cpu = None
@@ -323,7 +344,7 @@ def main():
     from muzero_hanoi_amd import engine, rng
     from muzero_hanoi_amd.networks import MuZeroNet
 
-    s0, s1 = mdist.shard_range(GB, world, rank)
+    s0, s1 = mdist.shard_range(GB, sworld, srank)
     B = s1 - s0  # this rank's roots
     torch.manual_seed(a.seed)
     net = MuZeroNet(3 * N, 6, 0.002, "cpu", TD_return=True)
@@ -334,7 +355,7 @@ def main():
     eng.load_weights(flat)
 
     # inputs for the GLOBAL batch in global root order, then this rank's contiguous shard
-    sl = lambda x: mdist.shard(x, world, rank)
+    sl = lambda x: mdist.shard(x, sworld, srank)
     obs = torch.from_numpy(sl(random_roots(N, GB, a.seed))).to(dev)
     noise, tie, u = rng.synthetic_draws(GB, deterministic=False, alpha=0.25, seed=a.seed)
     noise, tie, u = (torch.from_numpy(sl(x)).to(dev) for x in (noise, tie, u))
@@ -358,7 +379,10 @@ def main():
     sel_sum = float(out["sel_steps"].double().sum())
 
     # kernel-time probe: HIP events on the launch stream around each search launch
+    plan = search_plan(S, B, a.kernel, a.tile)
+    assert out["_plan"]["kernel"] == plan["kernel"], (out["_plan"], plan)  # the query names what launched
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    gevs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -369,11 +393,37 @@ def main():
         evs[k][1].record(stream)
         if gather:
             mdist.gather_results(out, GB, world)
+            gevs[k].record(stream)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+    gather_ms = float(np.mean([evs[k][1].elapsed_time(gevs[k]) for k in range(a.steps)])) if gather else None
+
+    # the instantiation training and acting searches run: the same roots with caller-given MinMaxStats
+    # bounds (run_mcts passes the MCTS instance's persistent bounds; fresh ones here), timed apart
+    mm = None
+    if not a.no_minmax_leg:
+        mm_in = torch.tensor([[-np.inf, np.inf]], dtype=torch.float64, device=dev).expand(B, 2).contiguous()
+        mout = eng.alloc_search_outputs(B, S)
+
+        def search_mm():
+            eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, minmax_in=mm_in, temperature=1.0,
+                       deterministic=False, discount=0.8, eps=0.25, out=mout, kernel=kern, tile=a.tile)
+
+        search_mm()
+        torch.cuda.synchronize(dev)
+        assert torch.equal(mout["visits"], out["visits"]), "fresh caller bounds changed the search"
+        mev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+        for s_, e_ in mev:
+            s_.record(stream)
+            search_mm()
+            e_.record(stream)
+        torch.cuda.synchronize(dev)
+        mm = {"kernel": mout["_plan"]["kernel"], "kernel_ms": float(np.mean([s_.elapsed_time(e_) for s_, e_ in mev])),
+              "what": "the same search with minmax_in given (fresh bounds: identical visits), the instantiation "
+                      "MCTS.run_mcts and batched self-play launch; 5 launches, HIP events"}
 
     # select / expand / backup alone: the replay instantiation of the same kernel on the same roots,
     # network outputs drawn like a random-init network's (near-uniform priors, small values)
@@ -403,7 +453,7 @@ def main():
         torch.cuda.synchronize(dev)
         tree_ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in tev]))
         tb = tree_bytes(rsel, B, S, EXPAND_BYTES_REPLAY)
-        tree = {"bound": "hbm", "kernel": kernel_name(a.kernel, B)[1].format(r="true"),
+        tree = {"bound": "hbm", "kernel": rout["_plan"]["kernel"],
                 "bytes_per_launch": tb, "kernel_ms": tree_ms, "achieved": tb / (tree_ms * 1e-3) / 1e9,
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s", "sel_steps_per_sim": rsel / (B * S),
                 "frac": tb / (tree_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "traffic": None,
@@ -414,25 +464,37 @@ def main():
                         "own selection-step count; fused_tree_bytes_per_launch: the same count in the fused "
                         "search (540 B per expansion incl. the latent read/write)"}
 
+    dinfo = None
     if dist is not None:
-        t = torch.tensor([dt, kern_ms, tree["kernel_ms"] if tree else 0.0], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        # every rank's own figures, gathered (so a scaling record shows the ranks RCCL saw), then maxed
+        mine = torch.tensor([dt, kern_ms, tree["kernel_ms"] if tree else 0.0, gather_ms or 0.0, float(B)],
+                            dtype=torch.float64, device=dev)
+        allr = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+        dist.all_gather(allr, mine)
+        allr = torch.stack(allr).cpu().numpy()
+        dinfo = {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()),
+                 "gather_ms_per_step": {"max": float(allr[:, 3].max()), "min": float(allr[:, 3].min())} if gather else None,
+                 "kernel_ms_per_rank": [float(x) for x in allr[:, 1]],
+                 "roots_per_rank": [int(x) for x in allr[:, 4]],
+                 "step_wall_s_per_rank": [float(x) for x in allr[:, 0]],
+                 "what": "one process per rank; gather = the all_gather of every root's visits/action/root Q "
+                         "(HIP events around it on the launch stream, mean per step)"}
+        t = torch.tensor(allr.max(0), dtype=torch.float64)
         dt, kern_ms = float(t[0]), float(t[1])
         if tree:
             tree["kernel_ms"] = float(t[2])
             tree["achieved"] = tree["bytes_per_launch"] / (tree["kernel_ms"] * 1e-3) / 1e9
             tree["frac"] = tree["achieved"] / HBM_PEAK_GBPS
 
-    sims_total = GB * S * a.steps
+    sims_total = (GB if a.shard is None else B) * S * a.steps
     value = sims_total / dt
     flops_launch = B * (S * MLP_FLOP_PER_SIM + root_flops(N))
     achieved = flops_launch / (kern_ms * 1e-3) / 1e12
-    kname = kernel_name(a.kernel, B)[1].format(r="false")
-    # waves sharing a SIMD: the wave kernel runs B / (16 NT) waves, two workgroups of 4 per CU at most;
-    # the cooperative kernel one 4-wave workgroup per CU
-    nt = 2 if kname.startswith("mzh_wave_kernel<2") else 1 if kname.startswith("mzh_wave_kernel<1") else 0
-    wps = 1 if nt == 0 else min(2, max(1, -(-B // (16 * nt * 1024))))
-    tkey = traffic_key(N, S, B, a.kernel)
+    kname = plan["kernel"]
+    wps = waves_per_simd(plan, B)
+    tkey = traffic_key(N, S, B, a.kernel, a.tile)
+    if mm is not None:
+        mm["frac"] = flops_launch / (mm["kernel_ms"] * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS
     tent, tnote = lookup_traffic(a.traffic_json, tkey)
     traffic = tent.get("hbm_bytes_per_launch") if tent else None
     if tree is not None and tent:
@@ -441,6 +503,9 @@ def main():
     if weak:
         workload = (f"weak scaling: {N}-disk, {B} roots per GPU ({GB} over {world} GPUs), {S} sims/move "
                     f"(not a BASELINE config unless N x roots matches one)")
+    elif a.shard is not None:
+        workload = (desc + f": rank {srank}'s shard of an N={sworld} job ({B} roots), run alone on one GPU "
+                    f"(value = this GPU's sims/s; the N={sworld} job's per-GPU work)")
     else:
         workload = desc + (f": {B} roots per GPU at N={world}" if world > 1 else
                            (" (the whole batch on one GPU)" if a.config in (2, 4) else ""))
@@ -458,7 +523,7 @@ def main():
         "dtype": "fp32",
         "data": f"synthetic: uniform random non-goal {N}-disk root states, random-init MuZeroNet(TD_return=True)",
         "config": {"workload": workload, "baseline_config": None if weak else a.config, "n_disks": N,
-                   "sims_per_move": S, "roots_per_gpu": B, "global_roots": GB,
+                   "sims_per_move": S, "roots_per_gpu": B, "global_roots": GB, "shard": a.shard,
                    "parallelism": f"dp{world} (independent roots, all_gather of visits/action/root Q)" if world > 1 else "dp1"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
@@ -472,8 +537,9 @@ def main():
                                           "what": "back-to-back MFMAs with distinct register operands at this "
                                                   "kernel's waves per SIMD (tools/micro/lds_a_probe.hip); "
                                                   "informational -- frac above is against the spec peak"},
-                     "tree": tree},
+                     "plan": plan, "with_minmax_in": mm, "tree": tree},
         "cpu_baseline": cpu,
+        "dist": dinfo,
         "build_id": _lib.build_id(),
     }
     if rank == 0:

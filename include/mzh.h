@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MZH_ABI_VERSION 2
+#define MZH_ABI_VERSION 3
 
 #define MZH_OK 0
 #define MZH_ERR_ARG (-1)         /* bad argument / shape (ValueError in Python)              */
@@ -165,10 +165,31 @@ typedef struct mzh_search_args {
    * exponent (integer exponents are exact products); without it the device pow is used, which can
    * differ from NumPy's vectorised pow in the last bit. */
   const double* pow_table;
+  /* HOST pointer (nullable): filled with the plan of the launched instantiation (below) */
+  struct mzh_search_plan* plan_out;
 } mzh_search_args;
+
+/* What a search launch runs: the kernel instantiation chosen from B, n_sims, the flags, the
+ * support and whether caller MinMaxStats bounds are given.  There is no reference counterpart (the
+ * reference runs one Python MCTS per root, MCTS/mcts.py:34-126); it exists so measurements name
+ * the kernel that actually ran. */
+typedef struct mzh_search_plan {
+  int32_t wave;                  /* 1: mzh_wave_kernel, 0: mzh_search_kernel (cooperative) */
+  int32_t roots_per_wave;        /* wave: 16 or 32; cooperative: tile / 4 (tree-phase roots per wave) */
+  int32_t roots_per_workgroup;   /* roots one workgroup owns */
+  int32_t threads_per_workgroup;
+  int32_t workgroups;            /* grid size */
+  int64_t smem_bytes;            /* dynamic LDS per workgroup */
+  char kernel[96];               /* the template instantiation as rocprofv3 names it, e.g.
+                                    "mzh_search_kernel<32, false, true, true, false>" */
+} mzh_search_plan;
 
 int mzh_search(mzh_engine* eng, const mzh_search_args* args, mzh_stream stream);
 int mzh_search_replay(mzh_engine* eng, const mzh_search_args* args, mzh_stream stream);
+/* The plan mzh_search (replay = 0) / mzh_search_replay (replay = 1) would launch for these
+ * arguments (has_minmax_in: args.minmax_in != NULL).  Host-only: needs no device and no engine. */
+int mzh_search_plan_query(int support, int B, int n_sims, uint32_t flags, int replay, int has_minmax_in,
+                          mzh_search_plan* out);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused training update.  Replaces Muzero._update (Muzero.py:209-274: represent, U unrolled

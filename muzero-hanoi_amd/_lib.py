@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "libmzh.so")
 LIB_PATH = os.environ.get("MZH_LIB") or DEFAULT_LIB  # MZH_LIB: diagnostic builds
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MZH_OK = 0
 MZH_ERR_ARG = -1
 MZH_ERR_HIP = -2
@@ -32,6 +32,16 @@ _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
 
 
+class SearchPlan(ctypes.Structure):
+    """mirror of struct mzh_search_plan (include/mzh.h)"""
+    _fields_ = [("wave", _i32), ("roots_per_wave", _i32), ("roots_per_workgroup", _i32),
+                ("threads_per_workgroup", _i32), ("workgroups", _i32), ("smem_bytes", ctypes.c_int64),
+                ("kernel", ctypes.c_char * 96)]
+
+    def as_dict(self):
+        return {f: (getattr(self, f).decode() if f == "kernel" else getattr(self, f)) for f, _ in self._fields_}
+
+
 class SearchArgs(ctypes.Structure):
     """mirror of struct mzh_search_args (include/mzh.h)"""
     _fields_ = [
@@ -41,6 +51,7 @@ class SearchArgs(ctypes.Structure):
         ("rp_root_pi", _vp), ("rp_sim", _vp),
         ("visits", _vp), ("root_q", _vp), ("minmax_out", _vp), ("extra_ties", _vp), ("action", _vp),
         ("pi", _vp), ("latent", _vp), ("latent_len", _vp), ("sel_steps", _vp), ("pow_table", _vp),
+        ("plan_out", ctypes.POINTER(SearchPlan)),
     ]
 
 
@@ -75,6 +86,8 @@ SIGNATURES = {
     "mzh_recurrent_inference": (ctypes.c_int, [_vp, ctypes.c_int] + [_vp] * 9 + [_vp]),
     "mzh_search": (ctypes.c_int, [_vp, ctypes.POINTER(SearchArgs), _vp]),
     "mzh_search_replay": (ctypes.c_int, [_vp, ctypes.POINTER(SearchArgs), _vp]),
+    "mzh_search_plan_query": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
+                                             ctypes.c_int, ctypes.POINTER(SearchPlan)]),
     "mzh_train_scratch_bytes": (ctypes.c_int, [ctypes.c_int] * 4 + [ctypes.POINTER(ctypes.c_size_t)]),
     "mzh_train_transpose": (ctypes.c_int, [ctypes.POINTER(TrainArgs), _vp]),
     "mzh_train_update": (ctypes.c_int, [ctypes.POINTER(TrainArgs), _vp]),
@@ -127,6 +140,14 @@ def check(status, what):
     if status in (MZH_ERR_ARG, MZH_ERR_TEMPERATURE):
         raise ValueError(msg)
     raise RuntimeError(msg)
+
+
+def search_plan(support, B, n_sims, flags=0, replay=False, minmax_in=False):
+    """the kernel instantiation mzh_search / mzh_search_replay would launch (host-only query)"""
+    out = SearchPlan()
+    check(lib().mzh_search_plan_query(int(support), int(B), int(n_sims), int(flags), 1 if replay else 0,
+                                      1 if minmax_in else 0, ctypes.byref(out)), "mzh_search_plan_query")
+    return out.as_dict()
 
 
 def device_count():

@@ -16,6 +16,7 @@ import logging
 import numpy as np
 import torch
 
+from .checkpoint import ablate_networks  # noqa: F401  (acting_ablations.py:29-45; one implementation)
 from .hanoi_utils import hanoi_solver
 from .selfplay import START_STATES
 
@@ -30,15 +31,6 @@ def get_starting_state(env, start=None):
     label = _LABELS[start]
     env.init_state_idx = env.states.index(START_STATES[label])
     return label
-
-
-def ablate_networks(reset_latent_policy, reset_latent_values, reset_latent_rwds, networks):
-    """Re-initialise the chosen heads with the network's own reset_param (networks.py:198-205)."""
-    for flag, head in ((reset_latent_policy, networks.policy_net), (reset_latent_values, networks.value_net),
-                       (reset_latent_rwds, networks.rwd_net)):
-        if flag:
-            head.apply(networks.reset_param)
-    return networks
 
 
 def _episode(env, start, networks, mcts, temperature, deterministic=False):

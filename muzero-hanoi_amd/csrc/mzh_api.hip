@@ -444,6 +444,65 @@ static KernelChoice choose_kernel(int B, uint32_t flags) {
   return {false, 0};
 }
 
+// every template argument of the launch (MzhSearchPlan); returns a status (capacity errors)
+static int make_plan(int B, int S, uint32_t flags, bool replay, int support, bool has_minmax, MzhSearchPlan* pl) {
+  const KernelChoice kc = choose_kernel(B, flags);
+  MzhSearchPlan q{};
+  q.wave = kc.wave ? 1 : 0;
+  q.nt = kc.nt;
+  q.replay = replay ? 1 : 0;
+  q.mmin = has_minmax ? 1 : 0;
+  if (kc.wave) {
+    if (mzh_wave_smem_bytes(S, kc.nt) > kMaxLds)
+      return fail(MZH_ERR_CAPACITY, "n_sims=%d exceeds the wave kernel's LDS table budget", S);
+    q.sup33 = support == 33;
+    q.mmin = 0;  // the wave kernel decides the exact normaliser per selection
+  } else {
+    q.R = pick_tile(B, flags);
+    if (mzh_search_smem_bytes(q.R, S, false) > kMaxLds) q.R = 16;
+    if (mzh_search_smem_bytes(q.R, S, false) > kMaxLds)
+      return fail(MZH_ERR_CAPACITY, "n_sims=%d exceeds the LDS path budget", S);
+    // the one-hot columns go to LDS when they fit (never in the replay kernel, which runs no MLP)
+    q.ohl = !replay && mzh_search_smem_bytes(q.R, S, true) <= kMaxLds;
+    q.sup33 = replay || support == 33;
+  }
+  *pl = q;
+  return MZH_OK;
+}
+
+static void plan_info(const MzhSearchPlan& q, int B, int S, mzh_search_plan* out) {
+  memset(out, 0, sizeof(*out));
+  const char* tf[2] = {"false", "true"};
+  out->wave = q.wave;
+  if (q.wave) {
+    out->roots_per_wave = 16 * q.nt;
+    out->threads_per_workgroup = 256;
+    out->roots_per_workgroup = 4 * 16 * q.nt;
+    out->smem_bytes = (int64_t)mzh_wave_smem_bytes(S, q.nt);
+    snprintf(out->kernel, sizeof(out->kernel), "mzh_wave_kernel<%d, %s, %s>", q.nt, tf[q.replay], tf[q.sup33]);
+  } else {
+    out->roots_per_wave = q.R / 4;
+    out->threads_per_workgroup = MZH_THREADS;
+    out->roots_per_workgroup = q.R;
+    out->smem_bytes = (int64_t)mzh_search_smem_bytes(q.R, S, q.ohl);
+    snprintf(out->kernel, sizeof(out->kernel), "mzh_search_kernel<%d, %s, %s, %s, %s>", q.R, tf[q.replay], tf[q.ohl],
+             tf[q.sup33], tf[q.mmin]);
+  }
+  out->workgroups = (B + out->roots_per_workgroup - 1) / out->roots_per_workgroup;
+}
+
+extern "C" int mzh_search_plan_query(int support, int B, int n_sims, uint32_t flags, int replay, int has_minmax_in,
+                                     mzh_search_plan* out) {
+  if (!out) return fail(MZH_ERR_ARG, "out is NULL");
+  if (B < 1 || n_sims < 0 || n_sims > 32000 || (support != 33 && support != 1))
+    return fail(MZH_ERR_ARG, "search_plan: bad B=%d n_sims=%d support=%d", B, n_sims, support);
+  MzhSearchPlan q;
+  const int st = make_plan(B, n_sims, flags, replay != 0, support, has_minmax_in != 0, &q);
+  if (st) return st;
+  plan_info(q, B, n_sims, out);
+  return MZH_OK;
+}
+
 static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream stream, bool replay) {
   if (!eng || !a) return fail(MZH_ERR_ARG, "engine or args NULL");
   if (a->B < 0 || a->n_sims < 0) return fail(MZH_ERR_ARG, "B=%d n_sims=%d", a->B, a->n_sims);
@@ -462,17 +521,10 @@ static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream s
   }
   if (!a->deterministic && !a->action_u && a->action)
     return fail(MZH_ERR_ARG, "stochastic action selection needs action_u");
-  const KernelChoice kc = choose_kernel(a->B, a->flags);
-  const bool wave = kc.wave;
-  int R = pick_tile(a->B, a->flags);
-  if (wave) {
-    if (mzh_wave_smem_bytes(a->n_sims, kc.nt) > kMaxLds)
-      return fail(MZH_ERR_CAPACITY, "n_sims=%d exceeds the wave kernel's LDS table budget", a->n_sims);
-  } else {
-    if (mzh_search_smem_bytes(R, a->n_sims) > kMaxLds) R = 16;
-    if (mzh_search_smem_bytes(R, a->n_sims) > kMaxLds)
-      return fail(MZH_ERR_CAPACITY, "n_sims=%d exceeds the LDS path budget", a->n_sims);
-  }
+  MzhSearchPlan pl;
+  const int st = make_plan(a->B, a->n_sims, a->flags, replay, eng->support, a->minmax_in != nullptr, &pl);
+  if (st) return st;
+  if (a->plan_out) plan_info(pl, a->B, a->n_sims, a->plan_out);
   DeviceGuard g(eng->device);
   if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
   MzhSearchParams p{};
@@ -485,8 +537,8 @@ static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream s
   p.visits = a->visits; p.root_q = a->root_q; p.minmax_out = a->minmax_out; p.extra_ties = a->extra_ties;
   p.action = a->action; p.pi = a->pi; p.latent = a->latent; p.latent_len = a->latent_len; p.sel_steps = a->sel_steps;
   p.pow_table = a->pow_table;
-  hipError_t e = wave ? mzh_launch_wave_search(kc.nt, replay, eng->wnet, p, (hipStream_t)stream)
-                      : mzh_launch_search(R, replay, eng->net, p, (hipStream_t)stream);
+  hipError_t e = pl.wave ? mzh_launch_wave_search(pl, eng->wnet, p, (hipStream_t)stream)
+                         : mzh_launch_search(pl, eng->net, p, (hipStream_t)stream);
   return e == hipSuccess ? MZH_OK : hip_fail(e, "search launch");
 }
 

@@ -114,8 +114,20 @@ struct MzhWNet {
   int support, in_dim;
 };
 
+// Every template argument of one search launch, decided once on the host (mzh_api.hip make_plan) and
+// used both to launch and to report the launched instantiation (mzh_search_plan_query)
+struct MzhSearchPlan {
+  int wave;    // 1: mzh_wave_kernel<nt, replay, sup33>; 0: mzh_search_kernel<R, replay, ohl, sup33, mmin>
+  int nt;      // wave kernel: 16-root column tiles per wave
+  int R;       // cooperative kernel: roots per workgroup
+  int replay;  // tree-only instantiation (recorded network outputs)
+  int ohl;     // cooperative: the dynamics one-hot columns in LDS
+  int sup33;   // 33-bin value / reward support (cooperative replay: always 1, one instantiation)
+  int mmin;    // cooperative: caller-given MinMaxStats bounds (subnormal max - min check)
+};
+
 size_t mzh_wave_smem_bytes(int S, int nt);
-hipError_t mzh_launch_wave_search(int nt, bool replay, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream);
-size_t mzh_search_smem_bytes(int R, int S);
-hipError_t mzh_launch_search(int R, bool replay, const MzhNet& net, const MzhSearchParams& p, hipStream_t stream);
+hipError_t mzh_launch_wave_search(const MzhSearchPlan& pl, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream);
+size_t mzh_search_smem_bytes(int R, int S, bool ohl);
+hipError_t mzh_launch_search(const MzhSearchPlan& pl, const MzhNet& net, const MzhSearchParams& p, hipStream_t stream);
 hipError_t mzh_launch_infer(int R, bool recurrent, const MzhNet& net, const MzhInferParams& p, hipStream_t stream);

@@ -236,35 +236,33 @@ static hipError_t launch_search_m(const MzhNet& net, const MzhSearchParams& p, h
   return hipGetLastError();
 }
 template <int R, bool REPLAY, bool OHL, bool SUP33>
-static hipError_t launch_search_s(const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
-  // caller-given bounds: the instantiation that checks for a subnormal max - min (never with OHL: the
-  // one-hot table is only an LDS placement choice)
-  if constexpr (!OHL) {
-    if (p.minmax_in) return launch_search_m<R, REPLAY, OHL, SUP33, true>(net, p, stream);
-  }
+static hipError_t launch_search_s(const MzhSearchPlan& pl, const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
+  // caller-given bounds: the instantiation that checks for a subnormal max - min (MzhTree::select)
+  if (pl.mmin) return launch_search_m<R, REPLAY, OHL, SUP33, true>(net, p, stream);
   return launch_search_m<R, REPLAY, OHL, SUP33, false>(net, p, stream);
 }
 template <int R, bool REPLAY, bool OHL>
-static hipError_t launch_search_t(const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
-  // the replay kernel never runs the network: one instantiation serves both supports
-  if (REPLAY || net.support == 33) return launch_search_s<R, REPLAY, OHL, true>(net, p, stream);
-  return launch_search_s<R, REPLAY, OHL, REPLAY>(net, p, stream);
+static hipError_t launch_search_t(const MzhSearchPlan& pl, const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
+  // the replay kernel never runs the network: one instantiation (SUP33 = true) serves both supports
+  if (REPLAY || pl.sup33) return launch_search_s<R, REPLAY, OHL, true>(pl, net, p, stream);
+  return launch_search_s<R, REPLAY, OHL, false>(pl, net, p, stream);
 }
 
-static const size_t kLdsBytes = 163840;  // 160 KB per CU (gfx950)
+// the LDS a search launch needs at tile R (ohl: with the dynamics one-hot columns in LDS)
+size_t mzh_search_smem_bytes(int R, int S, bool ohl) {
+  return R == 32 ? search_smem_bytes<32>(S, ohl) : search_smem_bytes<16>(S, ohl);
+}
 
-// the minimum LDS a search launch needs at this tile (one-hot columns left in HBM)
-size_t mzh_search_smem_bytes(int R, int S) { return R == 32 ? search_smem_bytes<32>(S, false) : search_smem_bytes<16>(S, false); }
-
-hipError_t mzh_launch_search(int R, bool replay, const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
-  if (R == 32) {
-    if (replay) return launch_search_t<32, true, false>(net, p, stream);
-    if (search_smem_bytes<32>(p.S, true) <= kLdsBytes && !p.minmax_in) return launch_search_t<32, false, true>(net, p, stream);
-    return launch_search_t<32, false, false>(net, p, stream);
+// the instantiation the plan names (mzh_api.hip make_plan decides every template argument)
+hipError_t mzh_launch_search(const MzhSearchPlan& pl, const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
+  if (pl.R == 32) {
+    if (pl.replay) return launch_search_t<32, true, false>(pl, net, p, stream);
+    if (pl.ohl) return launch_search_t<32, false, true>(pl, net, p, stream);
+    return launch_search_t<32, false, false>(pl, net, p, stream);
   }
-  if (replay) return launch_search_t<16, true, false>(net, p, stream);
-  if (search_smem_bytes<16>(p.S, true) <= kLdsBytes && !p.minmax_in) return launch_search_t<16, false, true>(net, p, stream);
-  return launch_search_t<16, false, false>(net, p, stream);
+  if (pl.replay) return launch_search_t<16, true, false>(pl, net, p, stream);
+  if (pl.ohl) return launch_search_t<16, false, true>(pl, net, p, stream);
+  return launch_search_t<16, false, false>(pl, net, p, stream);
 }
 
 template <int R>

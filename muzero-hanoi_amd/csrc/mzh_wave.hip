@@ -945,14 +945,13 @@ static hipError_t launch_wave_t(const MzhWNet& net, const MzhSearchParams& p, hi
 }
 
 template <int NT>
-static hipError_t launch_wave_nt(bool replay, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream) {
-  const bool sup33 = net.support == 33;
-  if (replay) return sup33 ? launch_wave_t<NT, true, true>(net, p, stream) : launch_wave_t<NT, true, false>(net, p, stream);
-  return sup33 ? launch_wave_t<NT, false, true>(net, p, stream) : launch_wave_t<NT, false, false>(net, p, stream);
+static hipError_t launch_wave_nt(const MzhSearchPlan& pl, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream) {
+  if (pl.replay) return pl.sup33 ? launch_wave_t<NT, true, true>(net, p, stream) : launch_wave_t<NT, true, false>(net, p, stream);
+  return pl.sup33 ? launch_wave_t<NT, false, true>(net, p, stream) : launch_wave_t<NT, false, false>(net, p, stream);
 }
 
-hipError_t mzh_launch_wave_search(int nt, bool replay, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream) {
-  return nt == 1 ? launch_wave_nt<1>(replay, net, p, stream) : launch_wave_nt<2>(replay, net, p, stream);
+hipError_t mzh_launch_wave_search(const MzhSearchPlan& pl, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream) {
+  return pl.nt == 1 ? launch_wave_nt<1>(pl, net, p, stream) : launch_wave_nt<2>(pl, net, p, stream);
 }
 
 #ifdef MZH_STAMPS

@@ -165,10 +165,7 @@ class Engine:
         a.eps = float(eps)
         a.temperature = float(temperature)
         a.deterministic = 1 if deterministic else 0
-        a.flags = (_lib.MZH_FLAG_NP1_UCB if np1_ucb else 0) | {None: 0, "coop": _lib.MZH_FLAG_KERNEL_COOP,
-                                                               "wave": _lib.MZH_FLAG_KERNEL_WAVE,
-                                                               "wave16": _lib.MZH_FLAG_KERNEL_WAVE16}[kernel]
-        a.flags |= {None: 0, 16: _lib.MZH_FLAG_COOP_TILE16, 32: _lib.MZH_FLAG_COOP_TILE32}[tile]
+        a.flags = search_flags(kernel, tile, np1_ucb)
         a.obs = ptr(dev(obs, torch.float32))
         a.noise = ptr(dev(noise, torch.float64))
         a.tie_idx = ptr(dev(tie_idx, torch.int32))
@@ -191,10 +188,21 @@ class Engine:
         if pt is not None:
             keep.append(pt)
         a.pow_table = ptr(pt)
+        plan = _lib.SearchPlan()
+        a.plan_out = ctypes.pointer(plan)
         fn = _lib.lib().mzh_search_replay if replay is not None else _lib.lib().mzh_search
         check(fn(self._h, ctypes.byref(a), self._stream()), "mzh_search")
         out["_keep"] = keep  # inputs stay alive until the caller is done with the async call
+        out["_plan"] = plan.as_dict()  # the instantiation the library launched
         return out
+
+
+def search_flags(kernel=None, tile=None, np1_ucb=False):
+    """mzh_search_args.flags for a kernel choice (None | "coop" | "wave" | "wave16") and coop tile"""
+    f = _lib.MZH_FLAG_NP1_UCB if np1_ucb else 0
+    f |= {None: 0, "auto": 0, "coop": _lib.MZH_FLAG_KERNEL_COOP, "wave": _lib.MZH_FLAG_KERNEL_WAVE,
+          "wave16": _lib.MZH_FLAG_KERNEL_WAVE16}[kernel]
+    return f | {None: 0, 16: _lib.MZH_FLAG_COOP_TILE16, 32: _lib.MZH_FLAG_COOP_TILE32}[tile]
 
 
 def pack_replay(replay):

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol(lib):
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(lib.SIGNATURES), "ctypes signature table out of sync with include/mzh.h"
-    assert L.mzh_abi_version() == lib.ABI_VERSION == 2
+    assert L.mzh_abi_version() == lib.ABI_VERSION == 3
 
 
 def _c_offsets(struct, fields, tmp_path):
@@ -63,8 +63,56 @@ def test_search_args_layout_matches_header(lib, tmp_path):
     hdr = open(HEADER).read()
     block = hdr[hdr.index("typedef struct mzh_search_args"):]
     block = block[:block.index("} mzh_search_args;")]
-    n_ptr_fields = len(re.findall(r"^\s+(?:const\s+)?\w+\*\s+\w+;", block, re.M))
-    assert n_ptr_fields == 17 == len(fields) - 7
+    n_ptr_fields = len(re.findall(r"^\s+(?:const\s+|struct\s+)?\w+\*\s+\w+;", block, re.M))
+    assert n_ptr_fields == 18 == len(fields) - 7
+
+
+def test_search_plan_layout_matches_header(lib, tmp_path):
+    """ctypes SearchPlan == struct mzh_search_plan"""
+    fields = [f[0] for f in lib.SearchPlan._fields_]
+    want = [getattr(lib.SearchPlan, f).offset for f in fields] + [ctypes.sizeof(lib.SearchPlan)]
+    assert _c_offsets("mzh_search_plan", fields, tmp_path) == want
+
+
+def test_search_plan_query_names_the_instantiations(lib):
+    """the host-only plan query (the code mzh_search launches from): kernel choice by batch size,
+    cooperative tile, the one-hot-in-LDS and caller-bounds template arguments, forced kernels / tiles,
+    the replay instantiation, capacity errors -- no device needed"""
+    from muzero_hanoi_amd import engine
+
+    P = lambda B, S=50, **kw: lib.search_plan(33, B, S, **kw)["kernel"]
+    assert P(65536) == "mzh_wave_kernel<2, false, true>"
+    assert P(53248) == "mzh_wave_kernel<2, false, true>"
+    assert P(53247) == "mzh_wave_kernel<1, false, true>"
+    assert P(8193) == "mzh_wave_kernel<1, false, true>"
+    assert P(8192) == "mzh_search_kernel<32, false, true, true, false>"
+    assert P(4097) == "mzh_search_kernel<32, false, true, true, false>"
+    assert P(4096) == "mzh_search_kernel<16, false, true, true, false>"
+    assert P(1) == "mzh_search_kernel<16, false, true, true, false>"
+    # caller MinMaxStats bounds (every run_mcts / self-play search): one-hot table still in LDS
+    assert P(4096, minmax_in=True) == "mzh_search_kernel<16, false, true, true, true>"
+    assert P(8192, minmax_in=True) == "mzh_search_kernel<32, false, true, true, true>"
+    assert P(65536, minmax_in=True) == "mzh_wave_kernel<2, false, true>"
+    # replay (tree-only): one instantiation for both supports, never the LDS one-hot table
+    assert P(8192, replay=True) == "mzh_search_kernel<32, true, false, true, false>"
+    assert lib.search_plan(1, 8192, 50, replay=True)["kernel"] == "mzh_search_kernel<32, true, false, true, false>"
+    assert lib.search_plan(1, 8192, 50)["kernel"] == "mzh_search_kernel<32, false, true, false, false>"
+    assert lib.search_plan(1, 65536, 50, replay=True)["kernel"] == "mzh_wave_kernel<2, true, false>"
+    # forced kernels / tiles
+    assert P(8192, flags=engine.search_flags(tile=16)) == "mzh_search_kernel<16, false, true, true, false>"
+    assert P(100, flags=engine.search_flags(tile=32)) == "mzh_search_kernel<32, false, true, true, false>"
+    assert P(100, flags=engine.search_flags("wave")) == "mzh_wave_kernel<2, false, true>"
+    assert P(70000, flags=engine.search_flags("coop")) == "mzh_search_kernel<32, false, true, true, false>"
+    assert P(70000, flags=engine.search_flags("wave16")) == "mzh_wave_kernel<1, false, true>"
+    # deep trees: the 32-root tile's LDS path budget gives way to 16 roots, then to a capacity error
+    big = lib.search_plan(33, 8192, 200)
+    assert big["roots_per_workgroup"] in (16, 32) and big["smem_bytes"] <= 163840
+    with pytest.raises(RuntimeError):
+        lib.search_plan(33, 4096, 20000)
+    pl = lib.search_plan(33, 8192, 50)
+    assert (pl["wave"], pl["roots_per_workgroup"], pl["workgroups"], pl["threads_per_workgroup"]) == (0, 32, 256, 256)
+    pl = lib.search_plan(33, 65536, 50)
+    assert (pl["wave"], pl["roots_per_wave"], pl["workgroups"]) == (1, 32, 512)
 
 
 def test_build_id_names_the_checked_out_sources(lib, tmp_path, monkeypatch):

@@ -15,7 +15,7 @@ def test_committed_traffic_has_the_default_bench_key():
     import bench
 
     key = bench.traffic_key(*bench.workload_shape(2)[:3])
-    assert key == "hanoi4_s50_roots65536_wave"
+    assert key == "hanoi4_s50_roots65536_mzh_wave_kernel<2,false,true>"
     doc = json.load(open(os.path.join(ROOT, "profiles", "traffic_latest.json")))
     assert key in doc["entries"]
     ent = doc["entries"][key]
@@ -23,13 +23,41 @@ def test_committed_traffic_has_the_default_bench_key():
 
 
 def test_traffic_keys_of_every_config_and_shard():
+    """the key names the fused instantiation the library's plan query reports -- the same host code
+    mzh_search launches from -- for every BASELINE config and per-GPU shard the driver runs"""
     import bench
 
-    assert bench.traffic_key(*bench.workload_shape(1)[:3]) == "hanoi4_s50_roots4096_coop"
-    assert bench.traffic_key(*bench.workload_shape(3)[:3]) == "hanoi4_s200_roots16384_wave16"
-    assert bench.traffic_key(*bench.workload_shape(2, world=8, rank=3)[:3]) == "hanoi4_s50_roots8192_coop"
-    assert bench.traffic_key(*bench.workload_shape(4, world=8)[:3]) == "hanoi7_s100_roots32768_wave16"
-    assert bench.traffic_key(*bench.workload_shape(2, roots_per_gpu=8192)[:3]) == "hanoi4_s50_roots8192_coop"
+    wave, wave16 = "mzh_wave_kernel<2,false,true>", "mzh_wave_kernel<1,false,true>"
+    c32, c16 = "mzh_search_kernel<32,false,true,true,false>", "mzh_search_kernel<16,false,true,true,false>"
+    want = {(1, 1): f"hanoi4_s50_roots4096_{c16}", (1, 2): f"hanoi4_s50_roots2048_{c16}",
+            (2, 1): f"hanoi4_s50_roots65536_{wave}", (2, 2): f"hanoi4_s50_roots32768_{wave16}",
+            (2, 4): f"hanoi4_s50_roots16384_{wave16}", (2, 8): f"hanoi4_s50_roots8192_{c32}",
+            (3, 1): f"hanoi4_s200_roots16384_{wave16}", (3, 2): f"hanoi4_s200_roots8192_{c16}",
+            (4, 1): f"hanoi7_s100_roots262144_{wave}", (4, 4): f"hanoi7_s100_roots65536_{wave}",
+            (4, 8): f"hanoi7_s100_roots32768_{wave16}"}
+    for (cfg, world), key in want.items():
+        for rank in range(world):
+            N, S, B, _ = bench.workload_shape(cfg, world=world, rank=rank)
+            assert bench.traffic_key(N, S, B) == key, (cfg, world, rank)
+    # a forced tile is part of the key (its PMC entry is not the default tile's)
+    assert bench.traffic_key(4, 50, 8192, tile=16) == f"hanoi4_s50_roots8192_{c16}"
+    assert bench.traffic_key(4, 50, 8192, minmax_in=True) == f"hanoi4_s50_roots8192_{c32[:-7]},true>"
+
+
+def test_bench_plan_is_the_library_plan():
+    """bench reports the library's plan (kernel, waves per SIMD) for every config x shard"""
+    import bench
+
+    from muzero_hanoi_amd import _lib
+
+    for cfg in (1, 2, 3, 4):
+        for world in (1, 2, 4, 8):
+            N, S, B, _ = bench.workload_shape(cfg, world=world)
+            pl = bench.search_plan(S, B)
+            assert pl == _lib.search_plan(33, B, S)
+            assert bench.waves_per_simd(pl, B) in (1, 2)
+            if pl["wave"] and pl["roots_per_wave"] == 32 and B >= 65536:
+                assert bench.waves_per_simd(pl, B) == 2
 
 
 def test_traffic_is_reported_only_for_the_profiled_build(tmp_path):
@@ -38,7 +66,7 @@ def test_traffic_is_reported_only_for_the_profiled_build(tmp_path):
     from muzero_hanoi_amd import _lib, build
 
     build.build()
-    key = "hanoi4_s50_roots65536_wave"
+    key = "hanoi4_s50_roots65536_mzh_wave_kernel<2,false,true>"
     p = tmp_path / "t.json"
     p.write_text(json.dumps({"entries": {key: {"build_id": "0" * 20, "hbm_bytes_per_launch": 1.0}}}))
     ent, note = bench.lookup_traffic(str(p), key)

@@ -193,7 +193,7 @@ def test_search_confident_heads_vs_oracle(mzh, oracle, kernel):
     eng = _engine(mzh, n, S, B, sup, flat)
     tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
     o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0, kernel=kernel)
-    o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+    o = {k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")}
     ref = oracle.search(n, S, obs, flat=flat, support=sup, noise=noise, tie_idx=tie, action_u=u, temperature=1.0)
     for k, rk in (("visits", "visits"), ("root_q", "rootQ"), ("action", "action"), ("sel_steps", "sel_steps"),
                   ("extra_ties", "extra_ties")):
@@ -240,7 +240,7 @@ def test_search_normalisation_exact_rerun_vs_oracle(mzh, oracle, kernel, tile):
     tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
     o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0, kernel=kernel,
                    tile=tile)
-    o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+    o = {k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")}
     ref = oracle.search(n, S, obs, flat=flat, support=sup, noise=noise, tie_idx=tie, action_u=u, temperature=1.0)
     for k, rk in (("visits", "visits"), ("root_q", "rootQ"), ("action", "action"), ("sel_steps", "sel_steps"),
                   ("extra_ties", "extra_ties")):
@@ -264,13 +264,13 @@ def _run_replay_case(mzh, g, kernel=None):
                            tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), minmax_in=mm,
                            temperature=T, deterministic=det, discount=float(g["discount"]), kernel=kernel)
             mm = o["minmax"].clone()
-            outs.append({k: v.cpu().numpy() for k, v in o.items() if k != "_keep"})
+            outs.append({k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")})
         return {k: np.concatenate([o[k] for o in outs]) for k in outs[0]}
     noise, tie, u = replay_draws(g)
     o = eng.search(S, replay=dict(root_pi=tt(rp["root_pi"]), pi=tt(rp["pi"]), reward=tt(rp["rwd"]), value=tt(rp["value"])),
                    tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=T, deterministic=det,
                    discount=float(g["discount"]), kernel=kernel)
-    return {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+    return {k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")}
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -304,7 +304,7 @@ def test_search_mlp_end_to_end_vs_oracle(mzh, oracle, case, kernel):
     tt = lambda a: None if a is None else torch.tensor(np.asarray(a), device=DEV)
     o = eng.search(S, obs=tt(g["obs"].astype(np.float32)), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u),
                    temperature=T, deterministic=det, discount=float(g["discount"]), kernel=kernel)
-    o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+    o = {k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")}
     ref = oracle.search(n, S, g["obs"], flat=flat, support=sup, noise=noise, tie_idx=tie, action_u=u,
                         temperature=T, deterministic=det, discount=float(g["discount"]))
     assert np.array_equal(o["visits"], ref["visits"])
@@ -334,7 +334,7 @@ def test_search_batched_vs_oracle_random_roots(mzh, oracle, B, S, n, kernel, til
     tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
     o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0, kernel=kernel,
                    tile=tile)
-    o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+    o = {k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")}
     nchk = min(B, 300)
     ref = oracle.search(n, S, obs[:nchk], flat=flat, support=sup, noise=noise[:nchk], tie_idx=tie[:nchk],
                         action_u=u[:nchk], temperature=1.0)
@@ -367,7 +367,7 @@ def test_search_wave_equals_coop_large_batch(mzh, oracle, B, S, n, td):
     for kernel in KERNELS:
         o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0,
                        kernel=kernel)
-        res[kernel] = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+        res[kernel] = {k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")}
     for kernel in KERNELS[1:]:
         for k in res["coop"]:
             assert np.array_equal(res["coop"][k], res[kernel][k], equal_nan=True), (kernel, k)
@@ -403,7 +403,7 @@ def test_search_deep_paths_replay(mzh, oracle, kernel, tile):
     tt = lambda a: None if a is None else torch.tensor(np.asarray(a), device=DEV)
     o = eng.search(S, replay=dict(root_pi=tt(root_pi), pi=tt(pi), reward=tt(rwd), value=tt(value)), tie_idx=tt(tie),
                    noise=None, action_u=None, temperature=1.0, deterministic=True, kernel=kernel, tile=tile)
-    o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+    o = {k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")}
     ref = oracle.search(n, S, obs, replay=rp, tie_idx=tie, temperature=1.0, deterministic=True)
     # every root's paths average deeper than any LDS path cache (max depth 120 = S)
     assert (ref["sel_steps"] / S).min() > 32 and ref["latent_len"].max() == S
@@ -435,7 +435,10 @@ def test_search_baseline_configs_full_size(mzh, oracle, B, S, n):
     eng = _engine(mzh, n, S, B, sup, flat)
     tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
     o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0)
-    o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+    from muzero_hanoi_amd import _lib
+
+    assert o["_plan"] == _lib.search_plan(sup, B, S)  # the host query names the launched instantiation
+    o = {k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")}
     assert np.all(o["visits"].sum(1) == S)
     assert np.all(np.isfinite(o["root_q"]))
     assert np.all(o["sel_steps"] >= S)  # every simulation descends at least one edge
@@ -460,7 +463,7 @@ def test_search_sharded_equals_whole_batch(mzh, oracle, B, S, n, W):
     tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
     eng = _engine(mzh, n, S, B, sup, flat)
     whole = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0)
-    whole = {k: v.cpu().numpy() for k, v in whole.items() if k != "_keep"}
+    whole = {k: v.cpu().numpy() for k, v in whole.items() if not k.startswith("_")}
     eng.close()
     shard = B // W
     es = _engine(mzh, n, S, shard, sup, flat)
@@ -468,6 +471,40 @@ def test_search_sharded_equals_whole_batch(mzh, oracle, B, S, n, W):
         sl = slice(r * shard, (r + 1) * shard)
         o = es.search(S, obs=tt(obs[sl]), tie_idx=tt(tie[sl]), noise=tt(noise[sl]), action_u=tt(u[sl]),
                       temperature=1.0)
-        o = {k: v.cpu().numpy() for k, v in o.items() if k != "_keep"}
+        o = {k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")}
         for k in ("visits", "root_q", "pi", "action", "sel_steps", "minmax", "extra_ties"):
             assert np.array_equal(o[k], whole[k][sl], equal_nan=True), (r, k)
+
+
+@pytest.mark.parametrize("B,tile", [(4096, None), (8192, None), (600, 32)])
+def test_search_caller_bounds_instantiation(mzh, oracle, B, tile):
+    """The instantiation run_mcts and batched self-play launch (caller MinMaxStats bounds; the
+    one-hot columns stay in LDS): fresh bounds give the same outputs as none, and a sample of roots
+    with carried-over bounds equals the oracle bit for bit."""
+    from muzero_hanoi_amd import _lib
+
+    S, n = 50, 4
+    flat, in_dim, sup = _weights(oracle, f"weights_N{n}_s0")
+    obs, noise, tie, u = _random_search_inputs(B, n, 3000 + B)
+    eng = _engine(mzh, n, S, B, sup, flat)
+    tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
+    kw = dict(obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0, tile=tile)
+    base = eng.search(S, **kw)
+    base = {k: v.cpu().numpy() for k, v in base.items() if not k.startswith("_")}
+    fresh = np.tile(np.array([[-np.inf, np.inf]]), (B, 1))
+    o = eng.search(S, minmax_in=tt(fresh), **kw)
+    flags = mzh.search_flags(tile=tile)
+    assert o["_plan"]["kernel"] == _lib.search_plan(sup, B, S, flags, minmax_in=True)["kernel"]
+    assert o["_plan"]["kernel"].endswith("true, true, true>")  # one-hot in LDS + caller bounds
+    o = {k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")}
+    for k in ("visits", "root_q", "pi", "action", "sel_steps", "minmax", "extra_ties"):
+        assert np.array_equal(o[k], base[k], equal_nan=True), k
+    # carried-over bounds (a second search of the same MCTS instances)
+    o2 = eng.search(S, minmax_in=tt(base["minmax"]), **kw)
+    o2 = {k: v.cpu().numpy() for k, v in o2.items() if not k.startswith("_")}
+    idx = _sample_idx(B, B)
+    ref = oracle.search(n, S, obs[idx], flat=flat, support=sup, noise=noise[idx], tie_idx=tie[idx],
+                        action_u=u[idx], temperature=1.0, minmax_in=base["minmax"][idx])
+    assert np.array_equal(o2["visits"][idx], ref["visits"])
+    assert np.array_equal(o2["root_q"][idx], ref["rootQ"])
+    assert np.array_equal(o2["minmax"][idx, 0], ref["mm_max"]) and np.array_equal(o2["minmax"][idx, 1], ref["mm_min"])

@@ -3,7 +3,7 @@ fused search (REPLAY = false) and its replay / tree-only instantiation (REPLAY =
 rocprofv3 average duration and the per-launch PMC values, HBM bytes corrected as
 MI355X_MICROARCH.md prescribes (FETCH_SIZE x 2 on gfx950, WRITE_SIZE as is; both in KB).
 
-  python tools/traffic.py gpurun_out TAG [--traffic-json profiles/traffic_latest.json] [--config K ...]
+  python tools/traffic.py gpurun_out TAG [--traffic-json profiles/traffic_latest.json]
 """
 import collections
 import csv
@@ -64,38 +64,73 @@ def summarise(root, tag):
     return out
 
 
+def bench_line(path):
+    """the last JSON line of a bench.py stdout capture (None if absent)"""
+    if not os.path.exists(path):
+        return None
+    for line in reversed(open(path).read().splitlines()):
+        line = line.strip()
+        if line.startswith("{"):
+            try:
+                return json.loads(line)
+            except ValueError:
+                continue
+    return None
+
+
 def main():
-    """python tools/traffic.py gpurun_out TAG [--traffic-json PATH] [bench options: --config K
-    --roots-per-gpu B --kernel X --disks N --sims S]: print the summary; with --traffic-json,
-    record it under the key bench.py computes for the same options (bench.traffic_key), with the
-    build id of the library that was profiled"""
+    """python tools/traffic.py gpurun_out TAG [--traffic-json PATH]: print the summary of the
+    profiled bench command (tools/prof.sh TAG) beside the same command's un-profiled bench line on the
+    same box; with --traffic-json, record the fused / tree kernels' PMC bytes under the workload key
+    the PROFILED bench line itself looked up (roofline.traffic_source.key), stamped with the build id
+    that run printed -- refused if the profiled and un-profiled runs, or this checkout, disagree on it"""
     import argparse
 
     sys.path.insert(0, ROOT)
-    import bench
 
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("tag")
     ap.add_argument("--traffic-json", default=None)
-    ap.add_argument("--config", type=int, default=2)
-    ap.add_argument("--roots-per-gpu", type=int, default=None)
-    ap.add_argument("--kernel", default="auto")
-    ap.add_argument("--disks", type=int, default=None)
-    ap.add_argument("--sims", type=int, default=None)
+    ap.add_argument("--expect-build", default=None,
+                    help="build id the profiled run must report (default: the checked-out sources' hash)")
     a = ap.parse_args()
     out = summarise(a.root, a.tag)
+    prof = bench_line(os.path.join(a.root, f"prof_{a.tag}_trace.log"))
+    plain = bench_line(os.path.join(a.root, f"prof_{a.tag}_plain.json"))
+    if plain is not None:
+        r = plain["roofline"]
+        out["unprofiled"] = {
+            "build_id": plain.get("build_id"), "kernel": r["kernel"], "kernel_ms_hip_events": r["kernel_ms"],
+            "ms_per_step": plain["ms_per_step"], "frac": r["frac"],
+            "tree_kernel_ms_hip_events": (r.get("tree") or {}).get("kernel_ms"),
+            "what": "the same bench command without rocprofv3, same box and build, run just before the profiled passes"}
+        f = out["fused"]
+        if f.get("avg_ns"):
+            out["unprofiled"]["rocprof_over_hip_events"] = f["avg_ns"] * 1e-6 / r["kernel_ms"]
+    if prof is not None:
+        out["profiled_bench"] = {"build_id": prof.get("build_id"), "kernel": prof["roofline"]["kernel"],
+                                 "key": prof["roofline"]["traffic_source"]["key"]}
     print(json.dumps(out, indent=1))
     if a.traffic_json:
-        from muzero_hanoi_amd import _lib
+        if prof is None:
+            raise SystemExit("no bench line in the profiled run's log: nothing to key the entry on")
+        if a.expect_build is None:
+            from muzero_hanoi_amd import build as _build
 
-        N, S, B, _ = bench.workload_shape(a.config, roots_per_gpu=a.roots_per_gpu, disks=a.disks, sims=a.sims)
-        key = bench.traffic_key(N, S, B, a.kernel)
+            a.expect_build = _build.source_hash()
+        bid = prof.get("build_id")
+        if bid != a.expect_build or (plain is not None and plain.get("build_id") != bid):
+            raise SystemExit(f"refusing to record: profiled build {bid}, un-profiled "
+                             f"{plain.get('build_id') if plain else None}, expected {a.expect_build}")
         f, t = out["fused"], out["tree"]
+        if f.get("kernel") and prof["roofline"]["kernel"] not in f["kernel"]:
+            raise SystemExit(f"the profiled kernel {f['kernel']} is not the bench's {prof['roofline']['kernel']}")
+        key = prof["roofline"]["traffic_source"]["key"]
         doc = json.load(open(a.traffic_json)) if os.path.exists(a.traffic_json) else {}
         entries = doc.get("entries", {})
         entries[key] = {
-            "build_id": _lib.build_id(), "kernel": f.get("kernel"), "avg_ns": f.get("avg_ns"),
+            "build_id": bid, "kernel": f.get("kernel"), "avg_ns": f.get("avg_ns"),
             "hbm_bytes_per_launch": f.get("hbm_bytes_per_launch"),
             "read_bytes_corrected": f.get("hbm_read_bytes_corrected"), "write_bytes": f.get("hbm_write_bytes"),
             "l2_hit_rate": f.get("l2_hit_rate"), "mfma_busy_frac": f.get("mfma_busy_frac"),
@@ -103,9 +138,10 @@ def main():
             "tree_kernel": t.get("kernel"), "tree_avg_ns": t.get("avg_ns"),
             "tree_hbm_bytes_per_launch": t.get("hbm_bytes_per_launch"),
             "tree_read_bytes_corrected": t.get("hbm_read_bytes_corrected"), "tree_write_bytes": t.get("hbm_write_bytes"),
+            "unprofiled_kernel_ms": (out.get("unprofiled") or {}).get("kernel_ms_hip_events"),
             "source": f"tools/prof.sh TAG={a.tag} + tools/traffic.py: rocprofv3 --kernel-trace --stats and separate "
                       "--pmc passes of the bench command; FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, "
-                      "per-dispatch sums, mean over dispatches"}
+                      "per-dispatch sums, mean over dispatches; key and build id from the profiled bench line"}
         json.dump({"what": "per-launch HBM bytes (PMC) of the bench workloads, keyed by bench.traffic_key; "
                            "bench.py reports an entry only when its build_id is the running library's",
                    "entries": entries}, open(a.traffic_json, "w"), indent=1)
