@@ -189,6 +189,18 @@ float orc_logits_to_value(const float* logits, int support) {
   return orc_signed_parabolic(sum8_tree(prod, support));
 }
 
+/* the expected scalar before the transform (networks.py:174-184: softmax, sum p_k * support_k) --
+ * the argument orc_logits_to_value hands to orc_signed_parabolic (test attribution only) */
+float orc_logits_expectation(const float* logits, int support) {
+  if (support == 1) return logits[0];
+  float p[ORC_MAXSUP];
+  softmax(logits, support, p);
+  int half = (support - 1) / 2;
+  float prod[ORC_MAXSUP];
+  for (int k = 0; k < support; ++k) prod[k] = p[k] * (float)(k - half);
+  return sum8_tree(prod, support);
+}
+
 /* normalize_h_state (networks.py:191-196) */
 static void normalize_h(float* h) {
   float mn = h[0], mx = h[0];

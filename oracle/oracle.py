@@ -43,6 +43,8 @@ def lib():
         L.orc_signed_parabolic.argtypes = [ctypes.c_float]
         L.orc_logits_to_value.restype = ctypes.c_float
         L.orc_logits_to_value.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.orc_logits_expectation.restype = ctypes.c_float
+        L.orc_logits_expectation.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.orc_markstein_mismatches.restype = ctypes.c_long
         L.orc_markstein_mismatches.argtypes = [ctypes.c_long, ctypes.c_uint64]
         L.orc_ucb_table.restype = ctypes.c_double
@@ -96,6 +98,23 @@ def load_weights_npz(path):
 
 def expf(x):
     return lib().orc_expf(float(x))
+
+
+def logits_to_value(logits):
+    """logits_to_transformed_expected_value of one logit row (networks.py:152-189)"""
+    lg = _c(logits, np.float32)
+    return float(lib().orc_logits_to_value(_p(lg), lg.size))
+
+
+def logits_expectation(logits):
+    """the pre-transform expected scalar of one logit row (networks.py:174-184)"""
+    lg = _c(logits, np.float32)
+    return float(lib().orc_logits_expectation(_p(lg), lg.size))
+
+
+def signed_parabolic(x):
+    """_signed_parabolic (networks.py:186-189) with a correctly rounded sqrt, fp32 op by op"""
+    return float(lib().orc_signed_parabolic(float(x)))
 
 
 def ucb_table(n):

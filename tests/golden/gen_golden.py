@@ -28,6 +28,8 @@ Fixtures (see tests/golden/README.md):
   bad_temperature.npz     run_mcts with invalid temperatures between valid ones (state after the raise)
   agree_<case>.npz        the reference's run_mcts (torch-CPU network) on 256-1024 roots per
                           (N, S) shape: visit histograms + root-level UCB gaps (near-tie report)
+  agree_n4s200_trace.npz  every network call (I/O, logits, pre-transform scalars, torch.sqrt
+                          arguments/results) of the roots the restated MLP's search disagrees on
 """
 import json
 import os
@@ -422,6 +424,104 @@ def gen_agreement(name, n, s, n_roots, seed, wseed=0, alpha=0.25, temperature=1.
                         obs=np.array(obs_all, np.float32), visits=np.array(visits, np.int32),
                         min_root_gap=np.array(min_gap, np.float64), zero_gaps=np.array(n_zero, np.int32),
                         min_deep_gap=np.array(deep, np.float64))
+
+
+def gen_agreement_trace(name, n, s, n_roots, seed, wseed=0, alpha=0.25, temperature=1.0, discount=0.8,
+                        controls=3):
+    """Every network call of the reference's run_mcts (torch-CPU MuZeroNet) for the roots of agree_<name>
+    whose visit histograms the oracle's search does not reproduce, plus `controls` agreeing roots:
+    inputs (parent latent, action), outputs (latent, reward, pi, value), the raw logits (policy 6,
+    value / reward 33, by forward hooks on the reference's own heads), the pre-transform scalars
+    (_transform_from_2hot) and every torch.sqrt argument / result inside _signed_parabolic
+    (networks.py:186-189) -- so the first simulation where the restated MLP leaves the reference, and
+    which operation moved it, can be read off (tests/test_parity_corners.py).  Same seeds and roots as
+    gen_agreement."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle import oracle as orc
+
+    g = np.load(os.path.join(HERE, f"agree_{name}.npz"))
+    w = {k: v for k, v in np.load(os.path.join(HERE, f"weights_N{n}_s{wseed}.npz")).items()}
+    flat = orc.flat_weights(w)
+    B = len(g["obs"])
+    noise, tie, u = [], [], []
+    for r in range(B):
+        np.random.seed(seed + r)
+        noise.append(np.random.dirichlet(np.ones(6, np.float32) * alpha))
+        tie.append(np.random.choice(np.arange(6)))
+        u.append(np.random.random_sample())
+    o = orc.search(n, s, g["obs"], flat=flat, support=33, noise=np.array(noise), tie_idx=np.array(tie),
+                   action_u=np.array(u), temperature=temperature, discount=discount)
+    bad = np.flatnonzero(~(o["visits"] == g["visits"]).all(1))
+    good = np.flatnonzero((o["visits"] == g["visits"]).all(1))[:controls]
+    roots = np.concatenate([bad, good]).astype(np.int32)
+
+    net = make_net(n, wseed, True)
+    cap = {}
+    hooks = [getattr(net, m).register_forward_hook(lambda mod, i, out, m=m: cap.setdefault(m, out.detach().clone()))
+             for m in ("policy_net", "value_net", "rwd_net")]
+    orig_t2h = net._transform_from_2hot
+
+    def t2h(probs, lo, hi):
+        x = orig_t2h(probs, lo, hi)
+        cap.setdefault("x", []).append(float(x.reshape(-1)[0]))
+        return x
+
+    net._transform_from_2hot = t2h
+    orig_sqrt = torch.sqrt
+
+    def sqrt(t, *a, **k):
+        r = orig_sqrt(t, *a, **k)
+        cap.setdefault("sqrt", []).append((float(t.reshape(-1)[0]), float(r.reshape(-1)[0])))
+        return r
+
+    recs = []
+
+    class Rec:
+        num_actions = net.num_actions
+
+        def _call(self, kind, fn, h, a):
+            cap.clear()
+            out = fn()
+            xs, sq = cap.get("x", []), cap.get("sqrt", [])
+            # recurrent: reward then value (dynamics before prediction, networks.py:104-107)
+            xr, xv = (xs[0], xs[1]) if kind == "r" else (0.0, xs[0])
+            sr, sv = (sq[0], sq[1]) if kind == "r" else ((0.0, 0.0), sq[0])
+            recs[-1].append(dict(
+                kind=kind, h_in=h, a=a, h=np.asarray(out[0], np.float32), rwd=float(out[1]),
+                pi=np.asarray(out[2], np.float32), v=float(out[3]),
+                pl=cap["policy_net"].numpy().reshape(-1), vl=cap["value_net"].numpy().reshape(-1),
+                rl=cap["rwd_net"].numpy().reshape(-1) if kind == "r" else np.zeros(33, np.float32),
+                xv=xv, xr=xr, sqrt_v=sv, sqrt_r=sr))
+            return out
+
+        def initial_inference(self, x):
+            return self._call("i", lambda: net.initial_inference(x), np.zeros(64, np.float32), -1)
+
+        def recurrent_inference(self, h, a):
+            return self._call("r", lambda: net.recurrent_inference(h, a), h.numpy().reshape(-1).copy(),
+                              int(a.argmax()))
+
+    torch.sqrt = sqrt
+    try:
+        for r in roots:
+            recs.append([])
+            np.random.seed(seed + int(r))
+            mcts = TracingMCTS(discount=discount, root_dirichlet_alpha=alpha, n_simulations=s, batch_s=256,
+                               device="cpu")
+            mcts.run_mcts(g["obs"][r].astype(np.float64), Rec(), temperature, False)
+            assert np.array_equal(mcts.last_visits, g["visits"][r]), "re-run differs from agree fixture"
+    finally:
+        torch.sqrt = orig_sqrt
+        for hk in hooks:
+            hk.remove()
+    st = lambda k, dt: np.array([[c[k] for c in rr] for rr in recs], dt)
+    np.savez_compressed(
+        os.path.join(HERE, f"agree_{name}_trace.npz"), n=n, s=s, seed=seed, roots=roots, n_bad=len(bad),
+        h_in=st("h_in", np.float32), a=st("a", np.int32), h=st("h", np.float32), rwd=st("rwd", np.float64),
+        pi=st("pi", np.float32), v=st("v", np.float64), pl=st("pl", np.float32), vl=st("vl", np.float32),
+        rl=st("rl", np.float32), xv=st("xv", np.float32), xr=st("xr", np.float32),
+        sqrt_v=st("sqrt_v", np.float32), sqrt_r=st("sqrt_r", np.float32))
+    return roots, len(bad)
 
 
 def gen_bad_temperature(n=3, s=25, seed=81, wseed=0):
@@ -841,6 +941,10 @@ def main():
     if "--agree-only" in sys.argv:
         for c in AGREE_CASES:
             gen_agreement(*c)
+        print(gen_agreement_trace(*AGREE_CASES[1]))
+        return
+    if "--agree-trace" in sys.argv:
+        print(gen_agreement_trace(*AGREE_CASES[1]))
         return
     if "--corners-only" in sys.argv:
         print("ucb rows differing", gen_ucb_rules())
@@ -860,6 +964,7 @@ def main():
     gen_bad_temperature()
     for c in AGREE_CASES:
         gen_agreement(*c)
+    gen_agreement_trace(*AGREE_CASES[1])
     for c in ACTING_CASES:
         gen_acting(*c)
     for c in ILLEGAL_CASES:

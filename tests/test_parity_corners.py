@@ -345,3 +345,172 @@ def test_subnormal_minmax_gap(oracle, kernel, tile):
     assert np.array_equal(o["root_q"].cpu().numpy(), ref["rootQ"])
     assert np.array_equal(o["minmax"].cpu().numpy()[:, 0], ref["mm_max"])
     assert np.array_equal(o["sel_steps"].cpu().numpy(), ref["sel_steps"])
+
+
+# ------------------------------- attribution of the one end-to-end disagreement (agree_n4s200 root 210)
+# agree_n4s200_trace.npz (gen_golden.gen_agreement_trace): every network call of the reference's
+# run_mcts for the roots whose oracle histograms differ from the reference's (root 210) and three
+# agreeing controls -- inputs, outputs, logits, the pre-transform scalars (_transform_from_2hot) and
+# every torch.sqrt argument / result inside _signed_parabolic (networks.py:152-189).
+def _trace_root(oracle, j):
+    g, t = golden("agree_n4s200.npz"), golden("agree_n4s200_trace.npz")
+    r = int(t["roots"][j])
+    flat, sup = _weights(oracle, "weights_N4_s0")
+    from muzero_hanoi_amd import rng
+
+    np.random.seed(int(g["seed"]) + r)
+    noise, tie, u = rng.predraw(1, deterministic=False, alpha=float(g["alpha"]))
+    return g, t, r, flat, noise, tie, u
+
+
+def _replay_rec(t, j, value=None):
+    """the reference's recorded outputs of traced root j as replay records (value optionally swapped)"""
+    return dict(root_pi=t["pi"][j][0][None], pi=t["pi"][j][1:][None], rwd=t["rwd"][j][1:][None].astype(np.float32),
+                value=(t["v"][j][1:] if value is None else value)[None].astype(np.float32))
+
+
+def _port_run(oracle, g, r, flat, net):
+    """py_port's tree (bit-exact to MCTS/node.py) on one root with the reference's global-stream seeding,
+    recording every root-level decision's float32 UCB scores"""
+    from oracle import py_port
+
+    rec = []
+    orig = py_port.Node.best_child
+
+    def best_child(self, pb_c_base, pb_c_init, discount, mm):
+        if self.parent is None:
+            q = np.array([mm.normalize(c.rwd + discount * c.Q()) if c.N > 0 else 0 for c in self.children], np.float32)
+            u = np.array([c.prior * ((math.log((self.N + pb_c_base + 1) / pb_c_base) + pb_c_init)
+                                     * math.sqrt(self.N) / (c.N + 1)) for c in self.children], np.float32)
+            rec.append((q + u, [c.W for c in self.children]))
+        return orig(self, pb_c_base, pb_c_init, discount, mm)
+
+    py_port.Node.best_child = best_child
+    try:
+        np.random.seed(int(g["seed"]) + r)
+        res = py_port.PortMCTS(float(g["discount"]), float(g["alpha"]), int(g["s"])).run_mcts(
+            g["obs"][r].astype(np.float64), net, float(g["temperature"]), False)
+    finally:
+        py_port.Node.best_child = orig
+    return res[3], rec
+
+
+class _OracleNet:
+    """the restated MLP (oracle, bit-equal to the GPU kernels) as a batch-1 network for py_port"""
+    num_actions = 6
+
+    def __init__(self, oracle, flat):
+        self.o, self.flat, self.calls = oracle, flat, []
+
+    def initial_inference(self, x):
+        d = self.o.initial_inference(self.flat, 12, 33, x.numpy()[None].astype(np.float32))
+        self.calls.append(d)
+        return d["h"][0], 0.0, d["pi"][0], float(d["value"][0])
+
+    def recurrent_inference(self, h, a):
+        d = self.o.recurrent_inference(self.flat, 12, 33, h.numpy()[None], np.array([int(a.argmax())]))
+        self.calls.append(d)
+        return d["h"][0], float(d["reward"][0]), d["pi"][0], float(d["value"][0])
+
+
+def test_n4s200_disagreement_attribution(oracle):
+    """Why root 210 of agree_n4s200 is the one histogram (of 256) the restated MLP's search does not
+    reproduce:
+      1. the tree is exact: the reference's recorded network outputs replayed through the oracle's
+         search give the reference's histogram (the GPU kernels: test_n4s200_trace_replay_gpu);
+      2. the first decision that differs is the root-level choice of simulation 54: the reference
+         picks child 0 by a float32 UCB margin of 7.2e-5 over child 4, the restated MLP's search
+         child 4 -- child 0's summed value W is 2.3e-3 lower on the restated side;
+      3. every output before it is equal except the policies (<= 4.5e-8, rounding noise) and ONE
+         reward: simulation 4's, one quantum (1.2e-4) of the signed-parabolic output lower.  Its
+         cause is the 33-bin expectation: the restated softmax + sum over the REFERENCE's own reward
+         logits gives x = -0.0087473392 where torch gave -0.0087471010 (a sum-order / exp difference
+         of 2.4e-7 on a cancelling sum), which lands x in the neighbouring output quantum;
+         torch.sqrt is correctly rounded at that call;
+      4. torch-CPU's not-correctly-rounded sqrt is not the cause: at the one value call where it is
+         1 ulp off (simulation 128, after the divergence), substituting the correctly rounded
+         result leaves the reference's histogram unchanged.
+    The three control roots agree and reach the same histogram by every route."""
+    g, t, r, flat, noise, tie, u = _trace_root(oracle, 0)
+    assert r == 210 and int(t["n_bad"]) == 1
+    kw = dict(noise=noise, tie_idx=tie, action_u=u, temperature=1.0, discount=0.8)
+    obs = g["obs"][r][None]
+    # 1. tree exactness
+    o = oracle.search(4, 200, obs, replay=_replay_rec(t, 0), **kw)
+    assert np.array_equal(o["visits"][0], g["visits"][r])
+    e2e = oracle.search(4, 200, obs, flat=flat, support=33, **kw)["visits"][0]
+    assert not np.array_equal(e2e, g["visits"][r])
+    # 2. first diverging decision (py_port tree, reference outputs vs the restated MLP)
+    from oracle import py_port
+
+    vis_ref, dec_ref = _port_run(oracle, g, r, flat, py_port.ReplayNet(t["pi"][0][0], t["pi"][0][1:],
+                                                                    t["rwd"][0][1:], t["v"][0][1:]))
+    onet = _OracleNet(oracle, flat)
+    vis_orc, dec_orc = _port_run(oracle, g, r, flat, onet)
+    assert np.array_equal(vis_ref, g["visits"][r]) and np.array_equal(vis_orc, e2e)
+    picks = [(int(np.argmax(a[0])), int(np.argmax(b[0]))) for a, b in zip(dec_ref, dec_orc)]
+    first = next(i for i, (a, b) in enumerate(picks) if a != b)
+    assert first == 53 and picks[first] == (0, 4)  # decision of simulation 54
+    s_ref, s_orc = dec_ref[first][0], dec_orc[first][0]
+    gap_ref, gap_orc = float(s_ref[0]) - float(s_ref[4]), float(s_orc[0]) - float(s_orc[4])
+    dW0 = dec_orc[first][1][0] - dec_ref[first][1][0]
+    print(f"simulation 54: reference UCB(child 0) - UCB(child 4) = {gap_ref:.3g}, restated {gap_orc:.3g}; "
+          f"child 0 W differs by {dW0:.3g}")
+    assert 0 < gap_ref < 1e-4 and gap_orc < 0 and -3e-3 < dW0 < -2e-3
+    # 3. what differs before it
+    oc = onet.calls[:54]
+    val = np.array([float(c["value"][0]) for c in oc], np.float32)
+    rwd = np.array([float(c["reward"][0]) for c in oc], np.float32)
+    pi = np.array([c["pi"][0] for c in oc], np.float32)
+    assert np.array_equal(val, t["v"][0][:54].astype(np.float32))
+    assert float(np.abs(pi - t["pi"][0][:54]).max()) < 1e-7
+    drw = np.flatnonzero(rwd[1:] != t["rwd"][0][1:54].astype(np.float32)) + 1
+    assert list(drw) == [4]
+    assert -1.3e-4 < float(rwd[4]) - float(t["rwd"][0][4]) < -1.1e-4
+    x_restated = np.float32(oracle.logits_expectation(t["rl"][0][4]))
+    x_torch = t["xr"][0][4]
+    print(f"simulation 4 reward: x from the reference's logits restated {x_restated!r}, torch {x_torch!r}")
+    assert x_restated != x_torch and abs(float(x_restated) - float(x_torch)) < 1e-6
+    assert np.float32(oracle.signed_parabolic(x_torch)) == np.float32(t["rwd"][0][4])
+    assert np.float32(oracle.signed_parabolic(x_restated)) == rwd[4]
+    sq = t["sqrt_r"][0][4]
+    assert np.sqrt(np.float32(sq[0])) == sq[1]  # torch's sqrt exact at that call
+    # 4. torch sqrt's 1-ulp misses: swapping in the correctly rounded value changes nothing
+    sv = t["sqrt_v"][0][1:]
+    miss = np.flatnonzero(np.sqrt(sv[:, 0].astype(np.float32)) != sv[:, 1])
+    assert list(miss + 1) == [128]
+    fixed = t["v"][0][1:].copy()
+    fixed[miss] = [oracle.signed_parabolic(x) for x in t["xv"][0][1:][miss]]
+    assert np.float32(fixed[miss][0]) != np.float32(t["v"][0][1:][miss][0])
+    o = oracle.search(4, 200, obs, replay=_replay_rec(t, 0, value=fixed), **kw)
+    assert np.array_equal(o["visits"][0], g["visits"][r])
+    # controls
+    for j in range(1, len(t["roots"])):
+        g, t, rc, flat, noise, tie, u = _trace_root(oracle, j)
+        kwc = dict(noise=noise, tie_idx=tie, action_u=u, temperature=1.0, discount=0.8)
+        o = oracle.search(4, 200, g["obs"][rc][None], replay=_replay_rec(t, j), **kwc)
+        assert np.array_equal(o["visits"][0], g["visits"][rc])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_n4s200_trace_replay_gpu(oracle, kernel):
+    """the traced roots (root 210 and the controls) with the reference's own recorded outputs
+    replayed through every kernel: the reference's histograms, bit for bit"""
+    import torch
+
+    from muzero_hanoi_amd.engine import Engine
+
+    t = golden("agree_n4s200_trace.npz")
+    J = len(t["roots"])
+    parts = [_trace_root(oracle, j) for j in range(J)]
+    g = parts[0][0]
+    noise = np.concatenate([p[4] for p in parts]); tie = np.concatenate([p[5] for p in parts])
+    u = np.concatenate([p[6] for p in parts])
+    rp = dict(root_pi=t["pi"][:, 0], pi=t["pi"][:, 1:], reward=t["rwd"][:, 1:].astype(np.float32),
+              value=t["v"][:, 1:].astype(np.float32))
+    eng = Engine(4, 200, J, 33)
+    tt = lambda a: torch.tensor(np.asarray(a), device="cuda")
+    o = eng.search(200, replay={k: tt(v) for k, v in rp.items()}, tie_idx=tt(tie), noise=tt(noise), action_u=tt(u),
+                   temperature=1.0, discount=0.8, kernel=kernel)
+    assert np.array_equal(o["visits"].cpu().numpy(), g["visits"][t["roots"]])
