@@ -51,6 +51,11 @@ SEL_BYTES, BACKUP_BYTES, EXPAND_BYTES = 124, 28, 540
 # new child statistics written (6 priors + the leaf reward = 28 B); no latent is read or written
 EXPAND_BYTES_REPLAY = 32 + 28
 
+# one dependent 128-B tree-block load (an 8-lane group's slot reads, L2-resident footprint, one wave per
+# SIMD on every CU) and the s_memtime rate: tools/micro/overlap_probe.hip, profiles/r04_overlap_probe.json
+TREE_LOAD_NS = None
+TREE_LOAD_FOOTPRINT = None
+
 METRIC = "MCTS sims/sec (node) 4-disk Hanoi, 50 sims/move, 65k root batch; 1/2/4/8 GPU"
 # BASELINE.json configs[1..4]: (disks, global roots, sims, description)
 CONFIGS = {
@@ -292,6 +297,32 @@ def lookup_traffic(path, key):
     return ent, "rocprofv3 PMC of this build (tools/prof.sh + tools/traffic.py)"
 
 
+def tree_latency_floor(sel_steps, S, plan, load_ns=None):
+    """A latency ceiling for select/backup (beside the HBM one): per simulation every lockstep group --
+    the cooperative kernel's workgroup of R roots, the wave kernel's wave of 16 NT roots -- waits for
+    its deepest root's selection, whose levels below the root are dependent block loads (the root level
+    is in LDS).  With d_r = sel_steps_r / S - 1 (root r's mean dependent loads per simulation) the
+    group needs at least S * max_r d_r loads in sequence; groups run concurrently on the GPU's slots
+    (256 CUs x 1 cooperative workgroup; 2,048 wave slots: 2 waves per SIMD).  Floor = rounds x S x
+    mean over groups of max_r d_r x the measured dependent-load latency.  max of the per-root MEANS is
+    below the mean of the per-simulation maxima, so this is a lower bound on the tree kernel's time."""
+    load_ns = TREE_LOAD_NS if load_ns is None else load_ns
+    if load_ns is None:
+        return None
+    d = np.asarray(sel_steps, np.float64) / S - 1.0
+    g = plan["roots_per_wave"] if plan["wave"] else plan["roots_per_workgroup"]
+    n = -(-len(d) // g)
+    dd = np.zeros(n * g)
+    dd[: len(d)] = d
+    gmax = dd.reshape(n, g).max(1)
+    slots = 2048 if plan["wave"] else 256
+    rounds = -(-n // slots)
+    floor_ms = rounds * S * float(gmax.mean()) * load_ns * 1e-6
+    return {"floor_ms": floor_ms, "groups": n, "roots_per_group": g, "rounds": rounds,
+            "mean_group_max_loads_per_sim": float(gmax.mean()), "mean_loads_per_sim": float(d.mean()),
+            "load_ns": load_ns, "load_footprint": TREE_LOAD_FOOTPRINT}
+
+
 def waves_per_simd(plan, B):
     """waves sharing a SIMD: the wave kernel runs B / roots_per_wave waves, two 4-wave workgroups per
     CU at most (1,024 SIMDs); the cooperative kernel one 4-wave workgroup per CU"""
@@ -458,12 +489,18 @@ def main():
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s", "sel_steps_per_sim": rsel / (B * S),
                 "frac": tb / (tree_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "traffic": None,
                 "fused_tree_bytes_per_launch": tree_bytes(sel_sum, B, S, EXPAND_BYTES),
+                "latency": tree_latency_floor(rout["sel_steps"].cpu().numpy(), S, rout["_plan"]),
                 "what": "select/expand/backup only: the search kernel's replay instantiation (same tree code, "
                         "network outputs read from HBM), same roots and draws; bytes = SURVEY.md 8d (124 B per "
                         "selection step, 28 B per backed-up node, 60 B per replayed expansion) with the kernel's "
                         "own selection-step count; fused_tree_bytes_per_launch: the same count in the fused "
                         "search (540 B per expansion incl. the latent read/write)"}
 
+    if tree is not None and tree["latency"] is not None:
+        tree["latency"]["frac"] = tree["latency"]["floor_ms"] / tree["kernel_ms"]
+        tree["latency"]["what"] = ("fraction of the tree kernel's HIP-event time that its deepest roots' dependent "
+                                   "block loads alone take (bench.tree_latency_floor); the HBM frac beside it "
+                                   "prices bytes, this one the load-latency chain")
     dinfo = None
     if dist is not None:
         # every rank's own figures, gathered (so a scaling record shows the ranks RCCL saw), then maxed
