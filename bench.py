@@ -53,8 +53,9 @@ EXPAND_BYTES_REPLAY = 32 + 28
 
 # one dependent 128-B tree-block load (an 8-lane group's slot reads, L2-resident footprint, one wave per
 # SIMD on every CU) and the s_memtime rate: tools/micro/overlap_probe.hip, profiles/r04_overlap_probe.json
-TREE_LOAD_NS = None
-TREE_LOAD_FOOTPRINT = None
+TREE_LOAD_NS = 136.1          # 16 MB footprint (L2-resident): the floor's latency
+TREE_LOAD_NS_MALL = 331.5     # 128 MB footprint (Infinity-Cache-resident), reported beside it
+TREE_LOAD_FOOTPRINT = "dependent 128-B block loads, 16 MB footprint over 256 CUs (L2-resident), one wave per SIMD"
 
 METRIC = "MCTS sims/sec (node) 4-disk Hanoi, 50 sims/move, 65k root batch; 1/2/4/8 GPU"
 # BASELINE.json configs[1..4]: (disks, global roots, sims, description)
@@ -318,7 +319,8 @@ def tree_latency_floor(sel_steps, S, plan, load_ns=None):
     slots = 2048 if plan["wave"] else 256
     rounds = -(-n // slots)
     floor_ms = rounds * S * float(gmax.mean()) * load_ns * 1e-6
-    return {"floor_ms": floor_ms, "groups": n, "roots_per_group": g, "rounds": rounds,
+    return {"floor_ms": floor_ms, "floor_ms_mall": floor_ms * TREE_LOAD_NS_MALL / load_ns,
+            "groups": n, "roots_per_group": g, "rounds": rounds,
             "mean_group_max_loads_per_sim": float(gmax.mean()), "mean_loads_per_sim": float(d.mean()),
             "load_ns": load_ns, "load_footprint": TREE_LOAD_FOOTPRINT}
 
@@ -446,15 +448,21 @@ def main():
         search_mm()
         torch.cuda.synchronize(dev)
         assert torch.equal(mout["visits"], out["visits"]), "fresh caller bounds changed the search"
-        mev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
-        for s_, e_ in mev:
-            s_.record(stream)
-            search_mm()
-            e_.record(stream)
+        # alternated with the plain search, so both see the same clocks
+        mev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(2)]
+               for _ in range(5)]
+        for pair in mev:
+            for fn, (s_, e_) in zip((search, search_mm), pair):
+                s_.record(stream)
+                fn()
+                e_.record(stream)
         torch.cuda.synchronize(dev)
-        mm = {"kernel": mout["_plan"]["kernel"], "kernel_ms": float(np.mean([s_.elapsed_time(e_) for s_, e_ in mev])),
+        t_plain = float(np.mean([p[0][0].elapsed_time(p[0][1]) for p in mev]))
+        t_mm = float(np.mean([p[1][0].elapsed_time(p[1][1]) for p in mev]))
+        mm = {"kernel": mout["_plan"]["kernel"], "kernel_ms": t_mm, "plain_kernel_ms_alternated": t_plain,
+              "ratio": t_mm / t_plain,
               "what": "the same search with minmax_in given (fresh bounds: identical visits), the instantiation "
-                      "MCTS.run_mcts and batched self-play launch; 5 launches, HIP events"}
+                      "MCTS.run_mcts and batched self-play launch; 5 launches alternated with 5 plain ones, HIP events"}
 
     # select / expand / backup alone: the replay instantiation of the same kernel on the same roots,
     # network outputs drawn like a random-init network's (near-uniform priors, small values)

@@ -83,3 +83,22 @@ def test_physical_core_count():
     cpus = sorted(os.sched_getaffinity(0))
     n = bench._physical_cores(cpus)
     assert 1 <= n <= len(cpus)
+
+
+def test_tree_latency_floor():
+    """the select/backup latency ceiling: deepest root per lockstep group x dependent-load latency"""
+    import numpy as np
+
+    import bench
+
+    S = 50
+    pl = bench.search_plan(S, 8192)  # cooperative: 32-root workgroups, 256 of them = one round
+    steps = np.full(8192, 3 * S)  # every root 3 levels per simulation = 2 dependent block loads
+    steps[::32] = 6 * S  # the deepest root of each group: 5 loads
+    f = bench.tree_latency_floor(steps, S, pl, load_ns=100.0)
+    assert f["roots_per_group"] == 32 and f["groups"] == 256 and f["rounds"] == 1
+    assert abs(f["mean_group_max_loads_per_sim"] - 5.0) < 1e-12
+    assert abs(f["floor_ms"] - S * 5 * 100e-6) < 1e-12
+    pw = bench.search_plan(S, 262144)  # wave kernel: 32-root waves, 8,192 waves = 4 rounds of 2,048 slots
+    f = bench.tree_latency_floor(np.full(262144, 2 * S), S, pw, load_ns=100.0)
+    assert f["roots_per_group"] == 32 and f["rounds"] == 4 and abs(f["floor_ms"] - 4 * S * 1 * 100e-6) < 1e-12
