@@ -425,6 +425,7 @@ static const size_t kMaxLds = 163840;
 // else the cooperative kernel (mzh_search.hip) whose 4 waves split every MLP layer of one 16- or
 // 32-root tile.  MZH_FLAG_KERNEL_* (or MZH_KERNEL=coop|wave|wave16) force one.
 static const int kWaveMinRoots = 53248, kWave16MinRoots = 8193;  // measured crossovers
+static const int kWaveWg8MinWaves = 1 << 30;  // phase-locked 8-wave workgroups: off until measured
 struct KernelChoice {
   bool wave;
   int nt;  // wave kernel: 16-root column tiles per wave
@@ -453,7 +454,18 @@ static int make_plan(int B, int S, uint32_t flags, bool replay, int support, boo
   q.replay = replay ? 1 : 0;
   q.mmin = has_minmax ? 1 : 0;
   if (kc.wave) {
-    if (mzh_wave_smem_bytes(S, kc.nt) > kMaxLds)
+    // 8-wave phase-locked workgroups once the batch gives two waves per SIMD (2,048 waves), else 4-wave
+    // workgroups (a one-wave-per-SIMD batch in 8-wave workgroups would leave half the CUs idle)
+    static const int envwg = [] {
+      const char* v = getenv("MZH_WAVE_WG");
+      return v ? atoi(v) : 0;
+    }();
+    const int waves = (B + 16 * kc.nt - 1) / (16 * kc.nt);
+    q.waves = waves >= kWaveWg8MinWaves ? 8 : 4;
+    if (envwg == 4 || envwg == 8) q.waves = envwg;
+    if (flags & MZH_FLAG_WAVE_WG8) q.waves = 8;
+    if (flags & MZH_FLAG_WAVE_WG4) q.waves = 4;
+    if (mzh_wave_smem_bytes(S, kc.nt, q.waves) > kMaxLds)
       return fail(MZH_ERR_CAPACITY, "n_sims=%d exceeds the wave kernel's LDS table budget", S);
     q.sup33 = support == 33;
     q.mmin = 0;  // the wave kernel decides the exact normaliser per selection
@@ -465,6 +477,16 @@ static int make_plan(int B, int S, uint32_t flags, bool replay, int support, boo
     // the one-hot columns go to LDS when they fit (never in the replay kernel, which runs no MLP)
     q.ohl = !replay && mzh_search_smem_bytes(q.R, S, true) <= kMaxLds;
     q.sup33 = replay || support == 33;
+    q.waves = 4;
+    if (q.R == 32) {
+      static const int env8 = [] {
+        const char* v = getenv("MZH_COOP_WAVES");
+        return v ? atoi(v) : 0;
+      }();
+      if (flags & MZH_FLAG_COOP_WAVES8) q.waves = 8;
+      else if (flags & MZH_FLAG_COOP_WAVES4) q.waves = 4;
+      else if (env8 == 8) q.waves = 8;
+    }
   }
   *pl = q;
   return MZH_OK;
@@ -476,17 +498,22 @@ static void plan_info(const MzhSearchPlan& q, int B, int S, mzh_search_plan* out
   out->wave = q.wave;
   if (q.wave) {
     out->roots_per_wave = 16 * q.nt;
-    out->threads_per_workgroup = 256;
-    out->roots_per_workgroup = 4 * 16 * q.nt;
-    out->smem_bytes = (int64_t)mzh_wave_smem_bytes(S, q.nt);
-    snprintf(out->kernel, sizeof(out->kernel), "mzh_wave_kernel<%d, %s, %s>", q.nt, tf[q.replay], tf[q.sup33]);
+    out->threads_per_workgroup = 64 * q.waves;
+    out->roots_per_workgroup = q.waves * 16 * q.nt;
+    out->smem_bytes = (int64_t)mzh_wave_smem_bytes(S, q.nt, q.waves);
+    snprintf(out->kernel, sizeof(out->kernel), "mzh_wave_kernel<%d, %s, %s, %d>", q.nt, tf[q.replay], tf[q.sup33],
+             q.waves);
   } else {
-    out->roots_per_wave = q.R / 4;
-    out->threads_per_workgroup = MZH_THREADS;
+    out->roots_per_wave = q.R / q.waves;
+    out->threads_per_workgroup = 64 * q.waves;
     out->roots_per_workgroup = q.R;
     out->smem_bytes = (int64_t)mzh_search_smem_bytes(q.R, S, q.ohl);
-    snprintf(out->kernel, sizeof(out->kernel), "mzh_search_kernel<%d, %s, %s, %s, %s>", q.R, tf[q.replay], tf[q.ohl],
-             tf[q.sup33], tf[q.mmin]);
+    if (q.waves == 8)
+      snprintf(out->kernel, sizeof(out->kernel), "mzh_search8_kernel<%s, %s, %s, %s>", tf[q.replay], tf[q.ohl],
+               tf[q.sup33], tf[q.mmin]);
+    else
+      snprintf(out->kernel, sizeof(out->kernel), "mzh_search_kernel<%d, %s, %s, %s, %s>", q.R, tf[q.replay],
+               tf[q.ohl], tf[q.sup33], tf[q.mmin]);
   }
   out->workgroups = (B + out->roots_per_workgroup - 1) / out->roots_per_workgroup;
 }

@@ -334,6 +334,21 @@ struct MlpSmem {
   int act[R];
 };
 
+// A 16-row view of a 32-row MlpSmem (rows 16h .. 16h + 15): the 8-wave cooperative kernel runs the 16-row
+// MLP schedule on each half with one 4-wave group per half (the MLP code takes any SM with these
+// members)
+struct MzhMlpView {
+  float *x, *hraw, *hidR, *hidP, *hidV, *lpol, *lval, *lrwd, *pi, *value, *reward;
+  int* act;
+};
+template <class SM>
+__device__ __forceinline__ MzhMlpView mzh_mlp_view(SM& sm, int h) {
+  const int r = 16 * h;
+  return MzhMlpView{sm.x + r * MZH_LD64,    sm.hraw + r * MZH_LD64, sm.hidR + r * MZH_LD256, sm.hidP + r * MZH_LD256,
+                    sm.hidV + r * MZH_LD256, sm.lpol + r * MZH_LDPOL, sm.lval + r * MZH_LDSUP, sm.lrwd + r * MZH_LDSUP,
+                    sm.pi + r * 8,           sm.value + r,           sm.reward + r,            sm.act + r};
+}
+
 struct MzhJob {
   const float* A;  // LDS, row stride lda
   const float4* W; // packed tile
@@ -874,7 +889,7 @@ __device__ __forceinline__ MzhChunk mzh_pred_tiles(SM& sm, const MzhNet& net, in
 template <int R, class SM, class BAR = MzhSyncBar>
 __device__ void mzh_mlp_initial(SM& sm, const MzhNet& net, int wave_in, int lane, BAR bar = BAR{}) {
   constexpr int MT = R / 16;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x & (MZH_THREADS - 1);  // within the 4-wave group (the 8-wave kernel runs two)
   const int wave = __builtin_amdgcn_readfirstlane(wave_in);
   floatx4 fa[16], fb[16];
   float ba[4], bb[4];
@@ -928,7 +943,7 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
                                                        floatx4* fa, float* ba, floatx4* fb, float* bb,
                                                        const float* onehot, BAR bar = BAR{}) {
   constexpr int MT = R / 16;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x & (MZH_THREADS - 1);  // within the 4-wave group (the 8-wave kernel runs two)
   const int wave = __builtin_amdgcn_readfirstlane(wave_in);  // wave-uniform -> chunk descriptors in SGPRs
   // Weight chunks alternate between the two fragment buffers, each refilled by the chain that
   // consumes it (ring, mzh_mma_store PT) with the chunk two steps ahead:
