@@ -3,3 +3,8 @@ set -e
 bash tools/pmc_mix.sh "" c2 "mzh_wave_kernel<2, false" > /dev/null
 bash tools/pmc_mix.sh "--config 2 --shard 0/4" s16k "mzh_wave_kernel<1, false" > /dev/null
 cat gpurun_out/pmcmix_c2.json gpurun_out/pmcmix_s16k.json
+# the cooperative 32-root tile's tree phase (replay instantiation: no MLP) on 4 vs 8 waves
+for cw in 4 8 4 8; do
+  MZH_COOP_WAVES=$cw timeout -k 10 120 python bench.py --config 2 --shard 0/8 --no-cpu-baseline --no-minmax-leg --steps 3 > gpurun_out/ab_tree_cw$cw.json 2>/dev/null
+  python -c "import json;d=json.load(open('gpurun_out/ab_tree_cw$cw.json'));t=d['roofline']['tree'];print('cw$cw',t['kernel'],'%.4f ms'%t['kernel_ms'])"
+done
