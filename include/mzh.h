@@ -49,8 +49,6 @@ extern "C" {
 #define MZH_FLAG_COOP_TILE32 32u /* cooperative kernel: 32 roots per workgroup (default for B > 4096) */
 #define MZH_FLAG_COOP_WAVES8 64u /* cooperative 32-root tile on 8 waves (two per SIMD, mzh_search8_kernel) */
 #define MZH_FLAG_COOP_WAVES4 128u /* cooperative 32-root tile on 4 waves (mzh_search_kernel<32, ...>) */
-#define MZH_FLAG_WAVE_WG8 256u /* wave kernel: 8-wave workgroups, phase-locked once per simulation */
-#define MZH_FLAG_WAVE_WG4 512u /* wave kernel: 4-wave workgroups, waves drift independently */
 
 typedef struct mzh_engine mzh_engine;
 typedef void* mzh_stream; /* hipStream_t */

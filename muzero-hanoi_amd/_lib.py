@@ -29,8 +29,6 @@ MZH_FLAG_COOP_TILE16 = 16  # cooperative kernel, 16 roots per workgroup
 MZH_FLAG_COOP_TILE32 = 32  # cooperative kernel, 32 roots per workgroup
 MZH_FLAG_COOP_WAVES8 = 64  # cooperative 32-root tile on 8 waves (mzh_search8_kernel)
 MZH_FLAG_COOP_WAVES4 = 128  # cooperative 32-root tile on 4 waves
-MZH_FLAG_WAVE_WG8 = 256  # wave kernel: 8-wave phase-locked workgroups
-MZH_FLAG_WAVE_WG4 = 512  # wave kernel: 4-wave workgroups
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32

@@ -425,7 +425,6 @@ static const size_t kMaxLds = 163840;
 // else the cooperative kernel (mzh_search.hip) whose 4 waves split every MLP layer of one 16- or
 // 32-root tile.  MZH_FLAG_KERNEL_* (or MZH_KERNEL=coop|wave|wave16) force one.
 static const int kWaveMinRoots = 53248, kWave16MinRoots = 8193;  // measured crossovers
-static const int kWaveWg8MinWaves = 1 << 30;  // phase-locked 8-wave workgroups: off until measured
 struct KernelChoice {
   bool wave;
   int nt;  // wave kernel: 16-root column tiles per wave
@@ -454,18 +453,8 @@ static int make_plan(int B, int S, uint32_t flags, bool replay, int support, boo
   q.replay = replay ? 1 : 0;
   q.mmin = has_minmax ? 1 : 0;
   if (kc.wave) {
-    // 8-wave phase-locked workgroups once the batch gives two waves per SIMD (2,048 waves), else 4-wave
-    // workgroups (a one-wave-per-SIMD batch in 8-wave workgroups would leave half the CUs idle)
-    static const int envwg = [] {
-      const char* v = getenv("MZH_WAVE_WG");
-      return v ? atoi(v) : 0;
-    }();
-    const int waves = (B + 16 * kc.nt - 1) / (16 * kc.nt);
-    q.waves = waves >= kWaveWg8MinWaves ? 8 : 4;
-    if (envwg == 4 || envwg == 8) q.waves = envwg;
-    if (flags & MZH_FLAG_WAVE_WG8) q.waves = 8;
-    if (flags & MZH_FLAG_WAVE_WG4) q.waves = 4;
-    if (mzh_wave_smem_bytes(S, kc.nt, q.waves) > kMaxLds)
+    q.waves = 4;
+    if (mzh_wave_smem_bytes(S, kc.nt) > kMaxLds)
       return fail(MZH_ERR_CAPACITY, "n_sims=%d exceeds the wave kernel's LDS table budget", S);
     q.sup33 = support == 33;
     q.mmin = 0;  // the wave kernel decides the exact normaliser per selection
@@ -500,9 +489,8 @@ static void plan_info(const MzhSearchPlan& q, int B, int S, mzh_search_plan* out
     out->roots_per_wave = 16 * q.nt;
     out->threads_per_workgroup = 64 * q.waves;
     out->roots_per_workgroup = q.waves * 16 * q.nt;
-    out->smem_bytes = (int64_t)mzh_wave_smem_bytes(S, q.nt, q.waves);
-    snprintf(out->kernel, sizeof(out->kernel), "mzh_wave_kernel<%d, %s, %s, %d>", q.nt, tf[q.replay], tf[q.sup33],
-             q.waves);
+    out->smem_bytes = (int64_t)mzh_wave_smem_bytes(S, q.nt);
+    snprintf(out->kernel, sizeof(out->kernel), "mzh_wave_kernel<%d, %s, %s>", q.nt, tf[q.replay], tf[q.sup33]);
   } else {
     out->roots_per_wave = q.R / q.waves;
     out->threads_per_workgroup = 64 * q.waves;

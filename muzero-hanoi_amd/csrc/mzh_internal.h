@@ -124,11 +124,10 @@ struct MzhSearchPlan {
   int ohl;     // cooperative: the dynamics one-hot columns in LDS
   int sup33;   // 33-bin value / reward support (cooperative replay: always 1, one instantiation)
   int mmin;    // cooperative: caller-given MinMaxStats bounds (subnormal max - min check)
-  int waves;   // cooperative: 4 (mzh_search_kernel) or 8 (mzh_search8_kernel, R = 32 only);
-               // wave kernel: waves per workgroup (4: two workgroups per CU; 8: one, phase-locked)
+  int waves;   // cooperative: 4 (mzh_search_kernel) or 8 (mzh_search8_kernel, R = 32 only)
 };
 
-size_t mzh_wave_smem_bytes(int S, int nt, int nw);
+size_t mzh_wave_smem_bytes(int S, int nt);
 hipError_t mzh_launch_wave_search(const MzhSearchPlan& pl, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream);
 size_t mzh_search_smem_bytes(int R, int S, bool ohl);
 hipError_t mzh_launch_search(const MzhSearchPlan& pl, const MzhNet& net, const MzhSearchParams& p, hipStream_t stream);

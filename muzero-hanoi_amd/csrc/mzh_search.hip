@@ -282,14 +282,8 @@ __global__ __launch_bounds__(MZH_THREADS8, 1) void mzh_search8_kernel(MzhNet net
   if (town) tree.template select<MMIN>(tr, tc, 0, rs);
   __syncthreads();
   for (int s = 0; s < S; ++s) {
-    if (!REPLAY) {
-      // the weight ring lives only inside the MLP (<= 256 registers at two waves per SIMD): the first two
-      // chunks are fetched here, not across the tree phase
-      floatx4 fa[16], fb[16];
-      float ba[4], bb[4];
-      mzh_mlp_fetch12<16>(mv, net, hw, lane, fa, ba, fb, bb);
-      mzh_mlp_recurrent_body<16, false, N2, false>(mv, net, hw, lane, fa, ba, fb, bb, OHL ? ohl : net.dyn0_onehot);
-    }
+    // one weight ring, live only inside the MLP (<= 256 registers at two waves per SIMD)
+    if (!REPLAY) mzh_mlp_recurrent_r1<16, N2>(mv, net, hw, lane, OHL ? ohl : net.dyn0_onehot);
     if (town) {
       const int r = tr, c = tc;
       MzhHeadOut ho;

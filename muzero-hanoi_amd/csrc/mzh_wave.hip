@@ -23,8 +23,7 @@
 #include "mzh_device.h"
 #include "mzh_internal.h"
 
-// waves per workgroup NW (template argument): 4 = two independent workgroups per CU, 8 = one workgroup of
-// two waves per SIMD held in phase by one barrier per simulation (both at 256 registers per wave)
+#define MZW_WAVES 4   // waves per workgroup; two workgroups per CU = two waves per SIMD (256 VGPRs)
 #define MZW_DC 16     // selection-path depths cached in LDS per root (deeper: HBM pathx)
 
 // tree block: identical to mzh_search.hip's MzhBlock (one 128-B line per expanded node)
@@ -363,13 +362,11 @@ __device__ __forceinline__ int mzw_pick_pair(const float (&u)[3], int half, int 
   return six ? tie : first;
 }
 
-// NW = 8 (a workgroup of 8 waves, two per SIMD): one workgroup barrier per simulation, before the MLP,
-// keeps the two waves of a SIMD in the same phase.  A v_mfma_f32_16x16x4_f32 stream holds the SIMD's
-// vector issue for its whole 32 cycles, so a wave in its tree phase beside a partner in its MLP makes
-// no progress (tools/micro/overlap_probe.hip): drifting waves pay MLP + MLP + tree + tree per SIMD,
-// waves in phase MLP + MLP + the longer tree phase (the tree phases, latency-bound, overlap each other).
-template <int NT, bool REPLAY, bool SUP33, int NW>
-__global__ __launch_bounds__(NW * 64, 8 / NW) void mzh_wave_kernel(MzhWNet net, MzhSearchParams p) {
+// The two waves a SIMD holds drift apart.  Phase-locking them (8-wave workgroups, one barrier per
+// simulation before the MLP) was measured 5-10% slower (profiles/r04_experiments.json): each
+// simulation then waits for the deepest of 256 roots.
+template <int NT, bool REPLAY, bool SUP33>
+__global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net, MzhSearchParams p) {
   constexpr int NOV = SUP33 ? 3 : 1;
   constexpr int ROOTS = 16 * NT;  // roots per wave
   const float* const noh[NT] = {};  // "no one-hot column" for the chains that take none
@@ -383,19 +380,15 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void mzh_wave_kernel(MzhWNet net, 
   const int g = lane >> 4, col = lane & 15;
 
   if (!REPLAY)
-    for (int i = tid; i < MZH_A * MZH_F; i += NW * 64) ohl[i] = net.oh[i];
+    for (int i = tid; i < MZH_A * MZH_F; i += MZW_WAVES * 64) ohl[i] = net.oh[i];
   double* inv = table + (S + 3);
-  for (int i = tid; i < S + 3; i += NW * 64) {
+  for (int i = tid; i < S + 3; i += MZW_WAVES * 64) {
     table[i] = i < S + 2 ? p.table[i] : 0.0;
     inv[i] = 1.0 / (double)i;  // IEEE division: correctly rounded
   }
   __syncthreads();  // the only barrier: from here on every wave runs independently
-  const int wr0 = (blockIdx.x * NW + wave) * ROOTS;
-  if (wr0 >= p.B) {  // wave-uniform: a wave past the batch (last workgroup) only keeps the barriers
-    if (NW == 8)
-      for (int s = 0; s < S; ++s) __syncthreads();
-    return;
-  }
+  const int wr0 = (blockIdx.x * MZW_WAVES + wave) * ROOTS;
+  if (wr0 >= p.B) return;  // wave-uniform
   MzwWave<ROOTS>& ws = wsa[wave];
   const double disc = p.discount;
   const bool noised = p.noise != nullptr;
@@ -856,7 +849,13 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void mzh_wave_kernel(MzhWNet net, 
     }
   };
 
+  // A/B builds only (-DMZW_PRIO_MODE): 0 the MLP phase at priority 1 (shipped), 1 the tree phases at
+  // priority 1 instead, 2 no priority change
+#ifndef MZW_PRIO_MODE
+#define MZW_PRIO_MODE 0
+#endif
   MZH_STAMP_DECL
+  if (MZW_PRIO_MODE == 1) __builtin_amdgcn_s_setprio(1);
   for (int s = 0; s < S; ++s) {
     MZH_STAMP(4);
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(rvalid && mmax > mmin && !(den >= 2.2250738585072014e-308)) != 0, 0))
@@ -864,11 +863,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void mzh_wave_kernel(MzhWNet net, 
     else
       phase_select(s, MzhBool<false>{});
     MZH_STAMP(0);
-    if (NW == 8) __syncthreads();  // both waves of every SIMD enter the MLP together
     // a wave in its matrix phase wins VALU issue arbitration over the co-resident wave's tree work
-    __builtin_amdgcn_s_setprio(1);
+    if (MZW_PRIO_MODE == 0) __builtin_amdgcn_s_setprio(1);
+    if (MZW_PRIO_MODE == 1) __builtin_amdgcn_s_setprio(0);
     phase_mlp(s);
-    __builtin_amdgcn_s_setprio(0);
+    if (MZW_PRIO_MODE == 0) __builtin_amdgcn_s_setprio(0);
+    if (MZW_PRIO_MODE == 1) __builtin_amdgcn_s_setprio(1);
     MZH_STAMP(1);
     phase_head(s);
     MZH_STAMP(2);
@@ -939,32 +939,30 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void mzh_wave_kernel(MzhWNet net, 
   }
 }
 
-size_t mzh_wave_smem_bytes(int S, int nt, int nw) {
-  return mzw_hdr_bytes(S) + (nt == 1 ? sizeof(MzwWave<16>) : sizeof(MzwWave<32>)) * nw;
+size_t mzh_wave_smem_bytes(int S, int nt) {
+  return mzw_hdr_bytes(S) + (nt == 1 ? sizeof(MzwWave<16>) : sizeof(MzwWave<32>)) * MZW_WAVES;
 }
 
-template <int NT, bool REPLAY, bool SUP33, int NW>
+template <int NT, bool REPLAY, bool SUP33>
 static hipError_t launch_wave_t(const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream) {
-  const size_t smem = mzh_wave_smem_bytes(p.S, NT, NW);
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mzh_wave_kernel<NT, REPLAY, SUP33, NW>),
+  const size_t smem = mzh_wave_smem_bytes(p.S, NT);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mzh_wave_kernel<NT, REPLAY, SUP33>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
-  const int per_wg = NW * 16 * NT;
+  const int per_wg = MZW_WAVES * 16 * NT;
   const int grid = (p.B + per_wg - 1) / per_wg;
-  hipLaunchKernelGGL((mzh_wave_kernel<NT, REPLAY, SUP33, NW>), dim3(grid), dim3(NW * 64), smem, stream, net, p);
+  hipLaunchKernelGGL((mzh_wave_kernel<NT, REPLAY, SUP33>), dim3(grid), dim3(MZW_WAVES * 64), smem, stream, net, p);
   return hipGetLastError();
 }
 
-template <int NT, int NW>
-static hipError_t launch_wave_nw(const MzhSearchPlan& pl, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream) {
-  if (pl.replay)
-    return pl.sup33 ? launch_wave_t<NT, true, true, NW>(net, p, stream) : launch_wave_t<NT, true, false, NW>(net, p, stream);
-  return pl.sup33 ? launch_wave_t<NT, false, true, NW>(net, p, stream) : launch_wave_t<NT, false, false, NW>(net, p, stream);
+template <int NT>
+static hipError_t launch_wave_nt(const MzhSearchPlan& pl, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream) {
+  if (pl.replay) return pl.sup33 ? launch_wave_t<NT, true, true>(net, p, stream) : launch_wave_t<NT, true, false>(net, p, stream);
+  return pl.sup33 ? launch_wave_t<NT, false, true>(net, p, stream) : launch_wave_t<NT, false, false>(net, p, stream);
 }
 
 hipError_t mzh_launch_wave_search(const MzhSearchPlan& pl, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream) {
-  if (pl.waves == 8) return pl.nt == 1 ? launch_wave_nw<1, 8>(pl, net, p, stream) : launch_wave_nw<2, 8>(pl, net, p, stream);
-  return pl.nt == 1 ? launch_wave_nw<1, 4>(pl, net, p, stream) : launch_wave_nw<2, 4>(pl, net, p, stream);
+  return pl.nt == 1 ? launch_wave_nt<1>(pl, net, p, stream) : launch_wave_nt<2>(pl, net, p, stream);
 }
 
 #ifdef MZH_STAMPS

@@ -81,10 +81,10 @@ def test_search_plan_query_names_the_instantiations(lib):
     from muzero_hanoi_amd import engine
 
     P = lambda B, S=50, **kw: lib.search_plan(33, B, S, **kw)["kernel"]
-    assert P(65536) == "mzh_wave_kernel<2, false, true, 4>"
-    assert P(53248) == "mzh_wave_kernel<2, false, true, 4>"
-    assert P(53247) == "mzh_wave_kernel<1, false, true, 4>"
-    assert P(8193) == "mzh_wave_kernel<1, false, true, 4>"
+    assert P(65536) == "mzh_wave_kernel<2, false, true>"
+    assert P(53248) == "mzh_wave_kernel<2, false, true>"
+    assert P(53247) == "mzh_wave_kernel<1, false, true>"
+    assert P(8193) == "mzh_wave_kernel<1, false, true>"
     assert P(8192) == "mzh_search_kernel<32, false, true, true, false>"
     assert P(4097) == "mzh_search_kernel<32, false, true, true, false>"
     assert P(4096) == "mzh_search_kernel<16, false, true, true, false>"
@@ -92,18 +92,18 @@ def test_search_plan_query_names_the_instantiations(lib):
     # caller MinMaxStats bounds (every run_mcts / self-play search): one-hot table still in LDS
     assert P(4096, minmax_in=True) == "mzh_search_kernel<16, false, true, true, true>"
     assert P(8192, minmax_in=True) == "mzh_search_kernel<32, false, true, true, true>"
-    assert P(65536, minmax_in=True) == "mzh_wave_kernel<2, false, true, 4>"
+    assert P(65536, minmax_in=True) == "mzh_wave_kernel<2, false, true>"
     # replay (tree-only): one instantiation for both supports, never the LDS one-hot table
     assert P(8192, replay=True) == "mzh_search_kernel<32, true, false, true, false>"
     assert lib.search_plan(1, 8192, 50, replay=True)["kernel"] == "mzh_search_kernel<32, true, false, true, false>"
     assert lib.search_plan(1, 8192, 50)["kernel"] == "mzh_search_kernel<32, false, true, false, false>"
-    assert lib.search_plan(1, 65536, 50, replay=True)["kernel"] == "mzh_wave_kernel<2, true, false, 4>"
+    assert lib.search_plan(1, 65536, 50, replay=True)["kernel"] == "mzh_wave_kernel<2, true, false>"
     # forced kernels / tiles
     assert P(8192, flags=engine.search_flags(tile=16)) == "mzh_search_kernel<16, false, true, true, false>"
     assert P(100, flags=engine.search_flags(tile=32)) == "mzh_search_kernel<32, false, true, true, false>"
-    assert P(100, flags=engine.search_flags("wave")) == "mzh_wave_kernel<2, false, true, 4>"
+    assert P(100, flags=engine.search_flags("wave")) == "mzh_wave_kernel<2, false, true>"
     assert P(70000, flags=engine.search_flags("coop")) == "mzh_search_kernel<32, false, true, true, false>"
-    assert P(70000, flags=engine.search_flags("wave16")) == "mzh_wave_kernel<1, false, true, 4>"
+    assert P(70000, flags=engine.search_flags("wave16")) == "mzh_wave_kernel<1, false, true>"
     # deep trees: the 32-root tile's LDS path budget gives way to 16 roots, then to a capacity error
     big = lib.search_plan(33, 8192, 200)
     assert big["roots_per_workgroup"] in (16, 32) and big["smem_bytes"] <= 163840

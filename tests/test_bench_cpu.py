@@ -15,7 +15,7 @@ def test_committed_traffic_has_the_default_bench_key():
     import bench
 
     key = bench.traffic_key(*bench.workload_shape(2)[:3])
-    assert key == "hanoi4_s50_roots65536_mzh_wave_kernel<2,false,true,4>"
+    assert key == "hanoi4_s50_roots65536_mzh_wave_kernel<2,false,true>"
     doc = json.load(open(os.path.join(ROOT, "profiles", "traffic_latest.json")))
     assert key in doc["entries"]
     ent = doc["entries"][key]
@@ -27,7 +27,7 @@ def test_traffic_keys_of_every_config_and_shard():
     mzh_search launches from -- for every BASELINE config and per-GPU shard the driver runs"""
     import bench
 
-    wave, wave16 = "mzh_wave_kernel<2,false,true,4>", "mzh_wave_kernel<1,false,true,4>"
+    wave, wave16 = "mzh_wave_kernel<2,false,true>", "mzh_wave_kernel<1,false,true>"
     c32, c16 = "mzh_search_kernel<32,false,true,true,false>", "mzh_search_kernel<16,false,true,true,false>"
     want = {(1, 1): f"hanoi4_s50_roots4096_{c16}", (1, 2): f"hanoi4_s50_roots2048_{c16}",
             (2, 1): f"hanoi4_s50_roots65536_{wave}", (2, 2): f"hanoi4_s50_roots32768_{wave16}",
@@ -66,7 +66,7 @@ def test_traffic_is_reported_only_for_the_profiled_build(tmp_path):
     from muzero_hanoi_amd import _lib, build
 
     build.build()
-    key = "hanoi4_s50_roots65536_mzh_wave_kernel<2,false,true,4>"
+    key = "hanoi4_s50_roots65536_mzh_wave_kernel<2,false,true>"
     p = tmp_path / "t.json"
     p.write_text(json.dumps({"entries": {key: {"build_id": "0" * 20, "hbm_bytes_per_launch": 1.0}}}))
     ent, note = bench.lookup_traffic(str(p), key)
