@@ -47,8 +47,6 @@ extern "C" {
 #define MZH_FLAG_KERNEL_WAVE16 8u /* force the wave-independent kernel, 16 roots per wave (default for 8192 < B < 53248) */
 #define MZH_FLAG_COOP_TILE16 16u /* cooperative kernel: 16 roots per workgroup (default for B <= 4096) */
 #define MZH_FLAG_COOP_TILE32 32u /* cooperative kernel: 32 roots per workgroup (default for B > 4096) */
-#define MZH_FLAG_COOP_WAVES8 64u /* cooperative 32-root tile on 8 waves (two per SIMD, mzh_search8_kernel) */
-#define MZH_FLAG_COOP_WAVES4 128u /* cooperative 32-root tile on 4 waves (mzh_search_kernel<32, ...>) */
 
 typedef struct mzh_engine mzh_engine;
 typedef void* mzh_stream; /* hipStream_t */

@@ -27,8 +27,6 @@ MZH_FLAG_KERNEL_WAVE = 4  # wave-independent kernel (mzh_wave.hip), 32 roots per
 MZH_FLAG_KERNEL_WAVE16 = 8  # wave-independent kernel, 16 roots per wave
 MZH_FLAG_COOP_TILE16 = 16  # cooperative kernel, 16 roots per workgroup
 MZH_FLAG_COOP_TILE32 = 32  # cooperative kernel, 32 roots per workgroup
-MZH_FLAG_COOP_WAVES8 = 64  # cooperative 32-root tile on 8 waves (mzh_search8_kernel)
-MZH_FLAG_COOP_WAVES4 = 128  # cooperative 32-root tile on 4 waves
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32

@@ -453,7 +453,6 @@ static int make_plan(int B, int S, uint32_t flags, bool replay, int support, boo
   q.replay = replay ? 1 : 0;
   q.mmin = has_minmax ? 1 : 0;
   if (kc.wave) {
-    q.waves = 4;
     if (mzh_wave_smem_bytes(S, kc.nt) > kMaxLds)
       return fail(MZH_ERR_CAPACITY, "n_sims=%d exceeds the wave kernel's LDS table budget", S);
     q.sup33 = support == 33;
@@ -466,16 +465,6 @@ static int make_plan(int B, int S, uint32_t flags, bool replay, int support, boo
     // the one-hot columns go to LDS when they fit (never in the replay kernel, which runs no MLP)
     q.ohl = !replay && mzh_search_smem_bytes(q.R, S, true) <= kMaxLds;
     q.sup33 = replay || support == 33;
-    q.waves = 4;
-    if (q.R == 32) {
-      static const int env8 = [] {
-        const char* v = getenv("MZH_COOP_WAVES");
-        return v ? atoi(v) : 0;
-      }();
-      if (flags & MZH_FLAG_COOP_WAVES8) q.waves = 8;
-      else if (flags & MZH_FLAG_COOP_WAVES4) q.waves = 4;
-      else if (env8 == 8) q.waves = 8;
-    }
   }
   *pl = q;
   return MZH_OK;
@@ -487,21 +476,17 @@ static void plan_info(const MzhSearchPlan& q, int B, int S, mzh_search_plan* out
   out->wave = q.wave;
   if (q.wave) {
     out->roots_per_wave = 16 * q.nt;
-    out->threads_per_workgroup = 64 * q.waves;
-    out->roots_per_workgroup = q.waves * 16 * q.nt;
+    out->threads_per_workgroup = 256;
+    out->roots_per_workgroup = 4 * 16 * q.nt;
     out->smem_bytes = (int64_t)mzh_wave_smem_bytes(S, q.nt);
     snprintf(out->kernel, sizeof(out->kernel), "mzh_wave_kernel<%d, %s, %s>", q.nt, tf[q.replay], tf[q.sup33]);
   } else {
-    out->roots_per_wave = q.R / q.waves;
-    out->threads_per_workgroup = 64 * q.waves;
+    out->roots_per_wave = q.R / 4;
+    out->threads_per_workgroup = MZH_THREADS;
     out->roots_per_workgroup = q.R;
     out->smem_bytes = (int64_t)mzh_search_smem_bytes(q.R, S, q.ohl);
-    if (q.waves == 8)
-      snprintf(out->kernel, sizeof(out->kernel), "mzh_search8_kernel<%s, %s, %s, %s>", tf[q.replay], tf[q.ohl],
-               tf[q.sup33], tf[q.mmin]);
-    else
-      snprintf(out->kernel, sizeof(out->kernel), "mzh_search_kernel<%d, %s, %s, %s, %s>", q.R, tf[q.replay],
-               tf[q.ohl], tf[q.sup33], tf[q.mmin]);
+    snprintf(out->kernel, sizeof(out->kernel), "mzh_search_kernel<%d, %s, %s, %s, %s>", q.R, tf[q.replay], tf[q.ohl],
+             tf[q.sup33], tf[q.mmin]);
   }
   out->workgroups = (B + out->roots_per_workgroup - 1) / out->roots_per_workgroup;
 }

@@ -334,21 +334,6 @@ struct MlpSmem {
   int act[R];
 };
 
-// A 16-row view of a 32-row MlpSmem (rows 16h .. 16h + 15): the 8-wave cooperative kernel runs the 16-row
-// MLP schedule on each half with one 4-wave group per half (the MLP code takes any SM with these
-// members)
-struct MzhMlpView {
-  float *x, *hraw, *hidR, *hidP, *hidV, *lpol, *lval, *lrwd, *pi, *value, *reward;
-  int* act;
-};
-template <class SM>
-__device__ __forceinline__ MzhMlpView mzh_mlp_view(SM& sm, int h) {
-  const int r = 16 * h;
-  return MzhMlpView{sm.x + r * MZH_LD64,    sm.hraw + r * MZH_LD64, sm.hidR + r * MZH_LD256, sm.hidP + r * MZH_LD256,
-                    sm.hidV + r * MZH_LD256, sm.lpol + r * MZH_LDPOL, sm.lval + r * MZH_LDSUP, sm.lrwd + r * MZH_LDSUP,
-                    sm.pi + r * 8,           sm.value + r,           sm.reward + r,            sm.act + r};
-}
-
 struct MzhJob {
   const float* A;  // LDS, row stride lda
   const float4* W; // packed tile
@@ -467,8 +452,7 @@ __device__ __forceinline__ MzhChunk mzh_chunk(const MzhLayer& L, int nt0, int nj
 
 // loads issued in consumption order (k-block major, the tiles of a k-block together), biases last:
 // the MFMAs of k-block 0 wait only for the oldest NJ fragments, not for the whole chunk
-// R1: slots in consumption order (slot kb * NJ + q), the single-ring layout of mzh_mma_store's R1 mode
-template <int NJ, int KB, bool ALL = false, bool R1 = false>
+template <int NJ, int KB, bool ALL = false>
 __device__ __forceinline__ void mzh_fetch(floatx4* f, float* bv, const MzhChunk& c, int lane) {
   static_assert(NJ * KB <= 16, "chunk too large");
 #pragma unroll
@@ -477,7 +461,7 @@ __device__ __forceinline__ void mzh_fetch(floatx4* f, float* bv, const MzhChunk&
     for (int q = 0; q < NJ; ++q) {
       if (ALL || q < c.nj) {
         const float4 t = c.w[q][kb * 64 + lane];
-        f[R1 ? kb * NJ + q : q * KB + kb] = floatx4{t.x, t.y, t.z, t.w};
+        f[q * KB + kb] = floatx4{t.x, t.y, t.z, t.w};
       }
     }
   }
@@ -505,12 +489,7 @@ struct MzhNoMid {
 // MID (optional): independent VALU / LDS work, mid(kb) placed in the region of k-block kb's MFMAs, so
 // it issues under their execution instead of on the phase's critical path (the latent normalisation
 // beside rwd0; it must neither read this chain's output nor write its A operand or its LDS output)
-// R1 (single ring): this chunk's fragments sit in consumption order (slot kb * NJ + q) and each slot,
-// once its MFMAs have issued, is refilled with the SAME slot of the next chunk `pc` (PNJ tiles, its
-// slots in consumption order too): every load gets about one chunk of MFMAs to land, with one
-// 16-fragment buffer instead of two (the two-waves-per-SIMD kernel's register budget)
-template <int MT, int NJ, int KB, bool ALL = false, int PT = 0, int PNB = 0, bool NAT = false, class MID = MzhNoMid,
-          bool R1 = false, int PNJ = 1>
+template <int MT, int NJ, int KB, bool ALL = false, int PT = 0, int PNB = 0, bool NAT = false, class MID = MzhNoMid>
 __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhChunk& c, const float* A, int lda,
                                               bool relu, const float* oht, const int* act, int lane,
                                               const MzhChunk* pc = nullptr, const floatx4* areg = nullptr,
@@ -521,10 +500,10 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
   const int r = lane & 15, g = lane >> 4;
   const float4* pw = PT > 0 ? pc->w[0] : nullptr;
   auto refill = [&](int slot) {
-    const float4 t = R1 ? pc->w[slot % PNJ][(slot / PNJ) * 64 + lane] : pw[slot * 64 + lane];
+    const float4 t = pw[slot * 64 + lane];
     f[slot] = floatx4{t.x, t.y, t.z, t.w};
   };
-  auto fs = [](int q, int kb) { return R1 ? kb * NJ + q : q * KB + kb; };
+  auto fs = [](int q, int kb) { return q * KB + kb; };
 #pragma unroll
   for (int slot = NJ * KB; slot < PT; ++slot) refill(slot);
   floatx4 acc[NJ][MT];
@@ -896,7 +875,7 @@ __device__ __forceinline__ MzhChunk mzh_pred_tiles(SM& sm, const MzhNet& net, in
 template <int R, class SM, class BAR = MzhSyncBar>
 __device__ void mzh_mlp_initial(SM& sm, const MzhNet& net, int wave_in, int lane, BAR bar = BAR{}) {
   constexpr int MT = R / 16;
-  const int tid = threadIdx.x & (MZH_THREADS - 1);  // within the 4-wave group (the 8-wave kernel runs two)
+  const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(wave_in);
   floatx4 fa[16], fb[16];
   float ba[4], bb[4];
@@ -950,7 +929,7 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
                                                        floatx4* fa, float* ba, floatx4* fb, float* bb,
                                                        const float* onehot, BAR bar = BAR{}) {
   constexpr int MT = R / 16;
-  const int tid = threadIdx.x & (MZH_THREADS - 1);  // within the 4-wave group (the 8-wave kernel runs two)
+  const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(wave_in);  // wave-uniform -> chunk descriptors in SGPRs
   // Weight chunks alternate between the two fragment buffers, each refilled by the chain that
   // consumes it (ring, mzh_mma_store PT) with the chunk two steps ahead:
@@ -1051,81 +1030,6 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
     bar();
   }
   MZH_STAMP(12);
-}
-
-// recurrent_inference with ONE 16-fragment weight ring (mzh_mma_store R1 mode: each chunk refills the
-// next chunk's fragments as it frees its slots) and no prefetch across the caller's tree phase: the
-// register budget of two waves per SIMD (mzh_search8_kernel).  Same chunks, same numerics as
-// mzh_mlp_recurrent_body<R, false, N2, false>.
-template <int R, int N2, class SM, class BAR = MzhSyncBar>
-__device__ __forceinline__ void mzh_mlp_recurrent_r1(SM& sm, const MzhNet& net, int wave_in, int lane,
-                                                     const float* onehot, BAR bar = BAR{}) {
-  constexpr int MT = R / 16;
-  const int tid = threadIdx.x & (MZH_THREADS - 1);
-  const int wave = __builtin_amdgcn_readfirstlane(wave_in);
-  const bool r2 = wave < N2;
-  const int P1 = r2 ? wave * (N2 + 4) : N2 * (N2 + 4) + (wave - N2) * (N2 + 8);
-  const int P2 = P1 + (r2 ? 0 : 4), P3 = P2 + 4;
-  const bool ht = mzh_has_head_tile<N2>(wave);
-  floatx4 f[16];
-  float bv[4];
-  const MzhChunk c_dyn0 = mzh_chunk(net.dyn0, wave * 4, 4, sm.hidP, MZH_LD256);
-  const MzhChunk c_dyn2 = mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64);
-  const MzhChunk c_rwd0 = mzh_chunk(net.rwd0, wave * 4, 4, sm.hidR, MZH_LD256);
-  mzh_fetch<4, 4, true, true>(f, bv, c_dyn0, lane);
-  mzh_mma_store<MT, 4, 4, true, 16, 1, false, MzhNoMid, true, 1>(f, bv, c_dyn0, sm.x, MZH_LD64, true, onehot, sm.act,
-                                                                  lane, &c_dyn2);  // dyn0 + one-hot + bias, relu
-  bar();
-  mzh_mma_store<MT, 1, 16, true, 16, 4, false, MzhNoMid, true, 4>(f, bv, c_dyn2, sm.hidP, MZH_LD256, false, nullptr,
-                                                                  nullptr, lane, &c_rwd0);  // dyn2 -> h'
-  bar();
-  MzhNormPass<R> norm;
-  bool slow = false;
-  auto mid = [&](int kb) {
-    if (kb == 0) norm.load(sm.hraw, tid);
-    if (kb == 1) norm.reduce();
-    if (kb == 2) slow = norm.template finish<false>(sm.x, tid);
-  };
-  const MzhChunk c_rwd2 = mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP);
-  const MzhChunk c_p1 = mzh_pred_tiles<R>(sm, net, P1, 4);
-  if (r2)
-    mzh_mma_store<MT, 4, 4, true, 16, 1, false, decltype(mid), true, 1>(f, bv, c_rwd0, sm.hraw, MZH_LD64, true, nullptr,
-                                                                        nullptr, lane, &c_rwd2, nullptr, mid);
-  else
-    mzh_mma_store<MT, 4, 4, true, 16, 4, false, decltype(mid), true, 4>(f, bv, c_rwd0, sm.hraw, MZH_LD64, true, nullptr,
-                                                                        nullptr, lane, &c_p1, nullptr, mid);
-  if (__builtin_expect(slow, 0)) norm.template finish<true>(sm.x, tid);
-  bar();
-  {
-    // the prediction chunks read the normalised latent from LDS (no register copy: registers)
-    const floatx4* ax = nullptr;
-    const MzhChunk c_p2 = mzh_pred_tiles<R>(sm, net, P2, 4);
-    const MzhChunk c_p3 = mzh_pred_tiles<R>(sm, net, P3, N2);
-    if (r2)
-      mzh_mma_store<MT, 1, 16, true, 16, 4, true, MzhNoMid, true, 4>(f, bv, c_rwd2, sm.hidR, MZH_LD256, false, nullptr,
-                                                                     nullptr, lane, &c_p2);  // rwd2 -> reward logits
-    else
-      mzh_mma_store<MT, 4, 4, true, 16, 4, false, MzhNoMid, true, 4>(f, bv, c_p1, sm.x, MZH_LD64, true, nullptr,
-                                                                     nullptr, lane, &c_p2, ax);
-    mzh_mma_store<MT, 4, 4, true, 4 * N2, N2, false, MzhNoMid, true, N2>(f, bv, c_p2, sm.x, MZH_LD64, true, nullptr,
-                                                                         nullptr, lane, &c_p3, ax);
-    if (ht) {
-      const MzhChunk c_h = mzh_head_chunk<R>(sm, net, wave);
-      mzh_mma_store<MT, N2, 4, true, 16, 1, false, MzhNoMid, true, 1>(f, bv, c_p3, sm.x, MZH_LD64, true, nullptr,
-                                                                      nullptr, lane, &c_h, ax);
-    } else {
-      mzh_mma_store<MT, N2, 4, true, 0, 0, false, MzhNoMid, true, 1>(f, bv, c_p3, sm.x, MZH_LD64, true, nullptr,
-                                                                     nullptr, lane, nullptr, ax);
-    }
-  }
-  bar();
-  if (ht) {
-    const MzhChunk c_h = mzh_head_chunk<R>(sm, net, wave);
-    float* hin = wave == 0 ? sm.hidP : sm.hidV;
-    mzh_mma_store<MT, 1, 16, true, 0, 0, true, MzhNoMid, true, 1>(f, bv, c_h, hin, MZH_LD256, false, nullptr, nullptr,
-                                                                  lane);  // pol2 / val2
-  }
-  bar();
 }
 
 template <int R>

@@ -124,7 +124,6 @@ struct MzhSearchPlan {
   int ohl;     // cooperative: the dynamics one-hot columns in LDS
   int sup33;   // 33-bin value / reward support (cooperative replay: always 1, one instantiation)
   int mmin;    // cooperative: caller-given MinMaxStats bounds (subnormal max - min check)
-  int waves;   // cooperative: 4 (mzh_search_kernel) or 8 (mzh_search8_kernel, R = 32 only)
 };
 
 size_t mzh_wave_smem_bytes(int S, int nt);

@@ -18,7 +18,9 @@
 // measured slower in both forms tried: two co-resident 16-root workgroups per CU
 // (<= 256 registers, no cross-phase prefetch) and a 512-thread workgroup whose waves 0-3 run the MLP
 // of one 16-root half while waves 4-7 run the other half's tree work (the co-resident tree work
-// took twice as long as alone).
+// took twice as long as alone) -- a v_mfma_f32_16x16x4_f32 stream holds its SIMD's vector issue, so a
+// partner wave's tree work stalls beside it (tools/micro/overlap_probe.hip).  The 32-root tile on 8
+// waves with both waves of a SIMD in the same phase lost 9% too.
 //
 // Per simulation: the MLP (all four waves split every layer's output tiles, activations in LDS),
 // one barrier, then each root's own 8-lane group runs -- with no further workgroup barrier -- the
@@ -177,141 +179,6 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
 }
 
 // ------------------------------------------------------------------------------------------
-// 8-wave cooperative kernel: 32 roots per workgroup, two waves per SIMD.  Waves 4h .. 4h + 3 run the
-// 16-row MLP schedule of mzh_search_kernel<16> on rows 16h .. 16h + 15 (a view of the 32-row LDS
-// block), so the two waves a SIMD holds issue the same chunk -- the same weight fragments, the
-// second wave's loads L1 hits -- on different rows, in the same phase (every barrier is the
-// workgroup's): each covers the other's dependent-MFMA, LDS and barrier latencies, and neither ever
-// runs tree work beside the other's f32 MFMAs (which would starve it: DESIGN.md §8, round 4).  The
-// tree phases spread the 32 roots over all 8 waves (4 roots, 32 lanes each).
-// ------------------------------------------------------------------------------------------
-#define MZH_THREADS8 512
-template <bool REPLAY, bool OHL, bool SUP33, bool MMIN>
-__global__ __launch_bounds__(MZH_THREADS8, 1) void mzh_search8_kernel(MzhNet net, MzhSearchParams p) {
-  constexpr int R = 32;
-  constexpr int DC = search_dc<R>();
-  using Smem = SearchSmem<R, DC>;
-  constexpr int RPW = R / 8;  // roots per wave in the tree phases
-  constexpr int N2 = SUP33 ? 3 : 1;
-  extern __shared__ __align__(16) unsigned char smem_raw[];
-  MlpSmem<R>& sm = *reinterpret_cast<MlpSmem<R>*>(smem_raw);
-  Smem& st = *reinterpret_cast<Smem*>(smem_raw + sizeof(MlpSmem<R>));
-  double* table = reinterpret_cast<double*>(smem_raw + sizeof(MlpSmem<R>) + sizeof(Smem));
-  double* inv = table + (p.S + 3);
-  uint16_t* path = reinterpret_cast<uint16_t*>(table + 2 * (p.S + 3));
-  float* ohl = reinterpret_cast<float*>(path + ((R * (p.S + 1) + 7) & ~7));
-
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int half = wave >> 2, hw = wave & 3;  // MLP: row half and wave within the half's 4-wave group
-  MzhMlpView mv = mzh_mlp_view(sm, half);
-  const int root0 = blockIdx.x * R;
-  const int nvalid = min(R, p.B - root0);
-  const int S = p.S;
-  const int PL = S + 1;
-  const double disc = p.discount;
-  const bool noised = p.noise != nullptr;
-  const int tr = wave * RPW + (lane >> 3), tc = lane & 7;
-  const bool tgroup = (lane >> 3) < RPW;
-
-  if (OHL)
-    for (int i = tid; i < MZH_A * MZH_F; i += MZH_THREADS8) ohl[i] = net.dyn0_onehot[i];
-  for (int i = tid; i < S + 3; i += MZH_THREADS8) {
-    table[i] = i < S + 2 ? p.table[i] : 0.0;
-    inv[i] = 1.0 / (double)i;
-  }
-  if (tid < R) {
-    const int r = tid;
-    st.rootN[r] = 0;
-    st.rootW[r] = 0.0;
-    st.firstTie[r] = 0;
-    st.extra[r] = 0;
-    st.steps[r] = 0;
-    st.depth[r] = 0;
-    st.tie[r] = (p.tie_idx && r < nvalid) ? p.tie_idx[root0 + r] : 0;
-    if (p.minmax_in && r < nvalid) {
-      mzh_mm_set(st.mm[r], p.minmax_in[2 * (root0 + r)], p.minmax_in[2 * (root0 + r) + 1]);
-    } else {
-      mzh_mm_set(st.mm[r], -__builtin_inf(), __builtin_inf());
-    }
-  }
-  // ---------------- root: initial_inference (mcts.py:49-50) ----------------
-  if (!REPLAY) {
-    for (int i = tid; i < R * p.kin; i += MZH_THREADS8) {
-      const int r = i / p.kin, k = i - r * p.kin;
-      sm.x[r * MZH_LD64 + mzh_kpos(k)] = (r < nvalid && k < p.in_dim) ? p.obs[(size_t)(root0 + r) * p.in_dim + k] : 0.0f;
-    }
-    __syncthreads();
-    mzh_mlp_initial<16>(mv, net, hw, lane);
-    for (int i = tid; i < R * MZH_H; i += MZH_THREADS8) {
-      const int r = i >> 6, k = i & 63;
-      if (r < nvalid) p.htree[((size_t)(root0 + r) * p.E) * MZH_H + k] = sm.x[r * MZH_LD64 + k];
-    }
-  } else {
-    if (tid < R * 8) {
-      const int r = tid >> 3, c = tid & 7;
-      sm.pi[r * 8 + c] = (r < nvalid && c < MZH_A) ? p.rp_root_pi[(size_t)(root0 + r) * MZH_A + c] : 0.0f;
-    }
-    __syncthreads();
-  }
-  if (tid < R * 8) {
-    const int r = tid >> 3, c = tid & 7;
-    MzhRootBlk& rb = st.root[r];
-    const float pr = (r < nvalid && c < MZH_A) ? sm.pi[r * 8 + c] : 0.0f;
-    rb.N[c] = 0;
-    rb.X[c] = -1;
-    rb.R[c] = 0.0f;
-    rb.W[c] = 0.0;
-    double v = (double)pr;
-    if (noised && r < nvalid && c < MZH_A) {
-      const float scaled = (float)(1.0 - p.eps) * pr;
-      v = (double)scaled + p.eps * p.noise[(size_t)(root0 + r) * MZH_A + c];
-    }
-    rb.P64[c] = v;
-  }
-  if (tid < R && tid >= nvalid) sm.act[tid] = 0;
-  __syncthreads();
-
-  MzhTree<R, DC, REPLAY, MlpSmem<R>> tree{p, st, sm, path, table, inv, root0, PL, lane, disc, noised};
-  auto group_sync = [&]() {
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-  };
-  MzhRootReg rs;
-  const bool town = tgroup && tr < nvalid;
-  if (town) rs.load(st, tr);
-  if (town) tree.template select<MMIN>(tr, tc, 0, rs);
-  __syncthreads();
-  for (int s = 0; s < S; ++s) {
-    // one weight ring, live only inside the MLP (<= 256 registers at two waves per SIMD)
-    if (!REPLAY) mzh_mlp_recurrent_r1<16, N2>(mv, net, hw, lane, OHL ? ohl : net.dyn0_onehot);
-    if (town) {
-      const int r = tr, c = tc;
-      MzhHeadOut ho;
-      if (!REPLAY) {
-        ho = mzh_heads_row<R, SUP33 ? 33 : 0, false>(sm, r, c, net.support, true);
-      } else {
-        const float* rec = p.rp_sim + ((size_t)s * p.B + root0 + r) * 8;
-        ho.pp = c < MZH_A ? rec[c] : 0.0f;
-        ho.reward = rec[6];
-        ho.value = rec[7];
-      }
-      tree.backup(r, c, s, rs, ho.value, ho.reward, ho.pp);
-      if (s + 1 < S) {
-        group_sync();
-        tree.template select<MMIN>(r, c, s + 1, rs);
-      }
-    }
-    __syncthreads();
-  }
-  if (town && tc == 0) rs.store(st, tr);
-  __syncthreads();
-  if (tid < R * 8) {
-    const int r = tid >> 3, c = tid & 7;
-    if (r < nvalid && c == 0) tree.results(r);
-  }
-}
-
-// ------------------------------------------------------------------------------------------
 // standalone batched inference kernels (MuZeroNet.initial_inference / recurrent_inference)
 // ------------------------------------------------------------------------------------------
 template <int R>
@@ -360,23 +227,12 @@ static size_t search_smem_bytes(int S, bool ohl) {
 }
 
 template <int R, bool REPLAY, bool OHL, bool SUP33, bool MMIN>
-static hipError_t launch_search_m(const MzhSearchPlan& pl, const MzhNet& net, const MzhSearchParams& p,
-                                  hipStream_t stream) {
+static hipError_t launch_search_m(const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
   const size_t smem = search_smem_bytes<R>(p.S, OHL);
-  const int grid = (p.B + R - 1) / R;
-  if constexpr (R == 32) {
-    if (pl.waves == 8) {
-      const void* fn = reinterpret_cast<const void*>(&mzh_search8_kernel<REPLAY, OHL, SUP33, MMIN>);
-      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-      if (e != hipSuccess) return e;
-      hipLaunchKernelGGL((mzh_search8_kernel<REPLAY, OHL, SUP33, MMIN>), dim3(grid), dim3(MZH_THREADS8), smem, stream,
-                         net, p);
-      return hipGetLastError();
-    }
-  }
   const void* fn = reinterpret_cast<const void*>(&mzh_search_kernel<R, REPLAY, OHL, SUP33, MMIN>);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
+  const int grid = (p.B + R - 1) / R;
   hipLaunchKernelGGL((mzh_search_kernel<R, REPLAY, OHL, SUP33, MMIN>), dim3(grid), dim3(MZH_THREADS), smem, stream, net,
                      p);
   return hipGetLastError();
@@ -384,8 +240,8 @@ static hipError_t launch_search_m(const MzhSearchPlan& pl, const MzhNet& net, co
 template <int R, bool REPLAY, bool OHL, bool SUP33>
 static hipError_t launch_search_s(const MzhSearchPlan& pl, const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
   // caller-given bounds: the instantiation that checks for a subnormal max - min (MzhTree::select)
-  if (pl.mmin) return launch_search_m<R, REPLAY, OHL, SUP33, true>(pl, net, p, stream);
-  return launch_search_m<R, REPLAY, OHL, SUP33, false>(pl, net, p, stream);
+  if (pl.mmin) return launch_search_m<R, REPLAY, OHL, SUP33, true>(net, p, stream);
+  return launch_search_m<R, REPLAY, OHL, SUP33, false>(net, p, stream);
 }
 template <int R, bool REPLAY, bool OHL>
 static hipError_t launch_search_t(const MzhSearchPlan& pl, const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {

@@ -849,13 +849,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
     }
   };
 
-  // A/B builds only (-DMZW_PRIO_MODE): 0 the MLP phase at priority 1 (shipped), 1 the tree phases at
-  // priority 1 instead, 2 no priority change
-#ifndef MZW_PRIO_MODE
-#define MZW_PRIO_MODE 0
-#endif
   MZH_STAMP_DECL
-  if (MZW_PRIO_MODE == 1) __builtin_amdgcn_s_setprio(1);
   for (int s = 0; s < S; ++s) {
     MZH_STAMP(4);
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(rvalid && mmax > mmin && !(den >= 2.2250738585072014e-308)) != 0, 0))
@@ -864,11 +858,10 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
       phase_select(s, MzhBool<false>{});
     MZH_STAMP(0);
     // a wave in its matrix phase wins VALU issue arbitration over the co-resident wave's tree work
-    if (MZW_PRIO_MODE == 0) __builtin_amdgcn_s_setprio(1);
-    if (MZW_PRIO_MODE == 1) __builtin_amdgcn_s_setprio(0);
+    // (measured against the tree phases first and against no priorities: profiles/r04_experiments.json)
+    __builtin_amdgcn_s_setprio(1);
     phase_mlp(s);
-    if (MZW_PRIO_MODE == 0) __builtin_amdgcn_s_setprio(0);
-    if (MZW_PRIO_MODE == 1) __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(0);
     MZH_STAMP(1);
     phase_head(s);
     MZH_STAMP(2);
