@@ -200,14 +200,29 @@ static int wperm_out(WOut kind, int ot, int r, int n_out) {
   return k < n_out ? k : -1;
 }
 struct PackedW {
-  size_t soff = 0, b1off = 0, b2off = 0;
+  size_t soff = 0, b1off = 0, b2off = 0, w32off = 0;
+  float b32 = 0.0f;
   int kb1 = 0, no = 0;
 };
+
+// bin 32 of a 33-bin head (MzhNet::rwd32 / MzhWMlp::w32): [16 blocks b][4 chains g] float4
+// {W2[32][16b + g], W2[32][16b + 4 + g], W2[32][16b + 8 + g], W2[32][16b + 12 + g]}
+static size_t pack_bin32(std::vector<float>& buf, const float* W2) {
+  while (buf.size() % 4) buf.push_back(0.0f);
+  const size_t off = buf.size();
+  buf.resize(buf.size() + 16 * 4 * 4, 0.0f);
+  const float* row = W2 + (size_t)32 * MZH_HIDDEN;
+  for (int b = 0; b < 16; ++b)
+    for (int g = 0; g < 4; ++g)
+      for (int t = 0; t < 4; ++t) buf[off + (size_t)(b * 4 + g) * 4 + t] = row[16 * b + 4 * t + g];
+  return off;
+}
 static PackedW pack_wmlp(std::vector<float>& buf, const float* W1, const float* b1, int K1, int ldw1, const float* W2,
                          const float* b2, int n_out, WOut kind) {
   PackedW P;
   P.kb1 = (K1 + 15) / 16;
-  P.no = (n_out + 15) / 16;
+  // a 33-bin head keeps bins 0..31 in two tiles; bin 32 goes to the vector chains (pack_bin32)
+  P.no = kind == WOUT_HEAD33 ? 2 : (n_out + 15) / 16;
   const int FR = P.kb1 + P.no;
   while (buf.size() % 4) buf.push_back(0.0f);
   P.soff = buf.size();
@@ -239,6 +254,10 @@ static PackedW pack_wmlp(std::vector<float>& buf, const float* W1, const float* 
       buf[P.b2off + 16 * ot + r] = row >= 0 ? b2[row] : 0.0f;
     }
   while (buf.size() % 4) buf.push_back(0.0f);
+  if (kind == WOUT_HEAD33) {
+    P.w32off = pack_bin32(buf, W2);
+    P.b32 = b2[32];
+  }
   return P;
 }
 
@@ -263,7 +282,9 @@ extern "C" int mzh_load_weights(mzh_engine* eng, const float* flat, size_t n_flo
   L[2] = pack_layer(buf, dyn0w, dyn0b, F, H, H + A);  // h part only (k < 64)
   L[3] = pack_layer(buf, dyn2w, dyn2b, H, F, F);
   L[4] = pack_layer(buf, rwd0w, rwd0b, F, H, H);
-  L[5] = pack_layer(buf, rwd2w, rwd2b, sup, F, F);
+  // 33-bin heads: bins 0..31 as MFMA tiles, bin 32 by vector chains (MzhNet::rwd32 / val32)
+  const int nhead = sup == 33 ? 32 : sup;
+  L[5] = pack_layer(buf, rwd2w, rwd2b, nhead, F, F);
   // pol0 and val0 weights back to back: the search kernel's prediction chunks take consecutive
   // tiles of this 32-tile strip and load them as one contiguous run (mzh_mma_store ring refill)
   pack_weights(buf, L[6], pol0w, F, H, H);
@@ -271,7 +292,7 @@ extern "C" int mzh_load_weights(mzh_engine* eng, const float* flat, size_t n_flo
   pack_bias(buf, L[6], pol0b, F);
   pack_bias(buf, L[8], val0b, F);
   L[7] = pack_layer(buf, pol2w, pol2b, A, F, F);
-  L[9] = pack_layer(buf, val2w, val2b, sup, F, F);
+  L[9] = pack_layer(buf, val2w, val2b, nhead, F, F);
   while (buf.size() % 4) buf.push_back(0.0f);
   const size_t ohoff = buf.size();
   buf.resize(buf.size() + (size_t)A * F);
@@ -315,6 +336,14 @@ extern "C" int mzh_load_weights(mzh_engine* eng, const float* flat, size_t n_flo
   if (n.val0.w != n.pol0.w + (size_t)n.pol0.nt * n.pol0.kb * 64)
     return fail(MZH_ERR_STATE, "pol0/val0 weights not contiguous");
   n.dyn0_onehot = base + ohoff;
+  n.rwd32 = n.val32 = nullptr;
+  n.rwd32b = n.val32b = 0.0f;
+  if (sup == 33) {  // the wave layout's bin-32 arrays serve both kernels
+    n.rwd32 = reinterpret_cast<const float4*>(base + WL[2].w32off);
+    n.val32 = reinterpret_cast<const float4*>(base + WL[4].w32off);
+    n.rwd32b = WL[2].b32;
+    n.val32b = WL[4].b32;
+  }
   n.support = sup;
   n.in_dim = in;
   auto mkw = [&](const PackedW& pw) {
@@ -324,6 +353,8 @@ extern "C" int mzh_load_weights(mzh_engine* eng, const float* flat, size_t n_flo
     m.b2 = base + pw.b2off;
     m.kb1 = pw.kb1;
     m.no = pw.no;
+    m.w32 = pw.w32off ? reinterpret_cast<const float4*>(base + pw.w32off) : nullptr;
+    m.b32 = pw.b32;
     return m;
   };
   MzhWNet& w = eng->wnet;

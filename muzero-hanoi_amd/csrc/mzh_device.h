@@ -296,9 +296,16 @@ struct MzhLayer {
   int kb, nt;
 };
 
+// Support 33: rwd2 / val2 hold bins 0..31 (two 16-row tiles); bin 32 -- which would cost a third
+// tile 15/16 padding -- is computed with vector FMAs as four k-ordered chains over k = g, g + 4, ...
+// (g = 0..3) combined ((p0 + p1) + (p2 + p3)), bias after (oracle/mzh_oracle.c linear_head).
+// rwd32 / val32: [16 blocks b][4 g] float4 {W[32][16b + g], W[32][16b + 4 + g], W[32][16b + 8 + g],
+// W[32][16b + 12 + g]}: the weights of chain g in its order (shared with the wave kernel, MzhWMlp::w32)
 struct MzhNet {
   MzhLayer rep0, rep2, dyn0, dyn2, rwd0, rwd2, pol0, pol2, val0, val2;
   const float* dyn0_onehot;  // [6][256]: dynamic_net.0.weight[:, 64 + a]
+  const float4 *rwd32, *val32;
+  float rwd32b, val32b;
   int support;               // 33 or 1
   int in_dim;                // 3N
 };
@@ -715,8 +722,36 @@ struct MzhHeadOut {
   float pp, value, reward;
 };
 template <int R, int SUP = 0, bool STORE = true, class SM>
-__device__ __forceinline__ MzhHeadOut mzh_heads_row(SM& sm, int row, int q, int support_in, bool recurrent) {
+__device__ __forceinline__ MzhHeadOut mzh_heads_row(SM& sm, const MzhNet& net, int row, int q, int support_in,
+                                                   bool recurrent) {
   const int support = SUP ? SUP : support_in;
+  // bin 32 of the reward (lanes 0-3) and value (lanes 4-7) logits: lane c of the quad runs chain c over
+  // hidden units 16b + 4j + c -- LDS positions 16b + 4c + j (k-block order), one ds_read_b128 per block
+  float l32r = 0.0f, l32v = 0.0f;
+  if (support == 33) {
+    const int hv = q >> 2, c = q & 3;
+    const float* hid = (hv ? sm.hidV : sm.hidR) + row * MZH_LD256 + 4 * c;
+    const float4* w = (hv ? net.val32 : net.rwd32) + c;
+    float acc = 0.0f;
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const floatx4 a4 = *reinterpret_cast<const floatx4*>(hid + 16 * b);
+      const float4 w4 = w[4 * b];
+      acc = __builtin_fmaf(a4[0], w4.x, acc);
+      acc = __builtin_fmaf(a4[1], w4.y, acc);
+      acc = __builtin_fmaf(a4[2], w4.z, acc);
+      acc = __builtin_fmaf(a4[3], w4.w, acc);
+    }
+    acc = acc + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc), 0xB1, 0xF, 0xF, true));  // p0+p1 | p2+p3
+    acc = acc + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc), 0x4E, 0xF, 0xF, true));  // (p0+p1)+(p2+p3)
+    const float l32 = acc + (hv ? net.val32b : net.rwd32b);
+    l32r = l32;  // valid on lanes 0-3
+    l32v = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(l32), 0x104, 0xF, 0xF, true));  // row_shl:4: lane 4 -> 0
+    if (STORE) {
+      if (q == 4) sm.lval[row * MZH_LDSUP + 32] = l32;
+      if (q == 0 && recurrent) sm.lrwd[row * MZH_LDSUP + 32] = l32;
+    }
+  }
   const float lraw = sm.lpol[row * MZH_LDPOL + q];
   const float lg = q < MZH_A ? lraw : -__builtin_inff();
   MzhHeadOut out{0.0f, 0.0f, 0.0f};
@@ -737,7 +772,8 @@ __device__ __forceinline__ MzhHeadOut mzh_heads_row(SM& sm, int row, int q, int 
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
       const int k = q + 8 * i;
-      const float raw = lv[h][k];
+      // bin 32 (lane 0, i = 4) from the vector chains above
+      const float raw = i == 4 ? (h ? l32r : l32v) : lv[h][k];
       e[h][i] = (h < nh && k < 33) ? raw : -__builtin_inff();
       m[h] = e[h][i] > m[h] ? e[h][i] : m[h];
     }
@@ -828,9 +864,9 @@ __device__ __forceinline__ MzhHeadOut mzh_heads_row(SM& sm, int row, int q, int 
 
 // all rows: 8 lanes per row, row = tid / 8 (32 rows over 256 threads)
 template <int R, class SM>
-__device__ __forceinline__ void mzh_heads_par(SM& sm, int support, bool recurrent, int tid) {
+__device__ __forceinline__ void mzh_heads_par(SM& sm, const MzhNet& net, bool recurrent, int tid) {
   const int row = tid >> 3, q = tid & 7;
-  if (row < R) mzh_heads_row<R>(sm, row, q, support, recurrent);
+  if (row < R) mzh_heads_row<R>(sm, net, row, q, net.support, recurrent);
 }
 
 // The per-wave chunk schedule of the prediction function (networks.py:140-150) on sm.x:
@@ -904,7 +940,7 @@ __device__ void mzh_mlp_initial(SM& sm, const MzhNet& net, int wave_in, int lane
   mzh_mma_store<MT, 1, 16, false, 0, 0, true>(fa, ba, c7, c7.out[0] == sm.lpol ? sm.hidP : sm.hidV, MZH_LD256, false,
                                             nullptr, nullptr, lane);
   bar();
-  mzh_heads_par<R>(sm, net.support, false, tid);
+  mzh_heads_par<R>(sm, net, false, tid);
   bar();
 }
 
@@ -1025,7 +1061,7 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
   MZH_STAMP(10);
   bar();
   if (HEADS) {
-    mzh_heads_par<R>(sm, net.support, true, tid);
+    mzh_heads_par<R>(sm, net, true, tid);
     MZH_STAMP(11);
     bar();
   }
@@ -1038,7 +1074,7 @@ __device__ void mzh_mlp_recurrent(MlpSmem<R>& sm, const MzhNet& net, int wave, i
   float ba[4], bb[4];
   mzh_mlp_fetch12<R>(sm, net, wave, lane, fa, ba, fb, bb);
   if (net.support == 33)
-    mzh_mlp_recurrent_body<R, false, 3, true>(sm, net, wave, lane, fa, ba, fb, bb, net.dyn0_onehot);
+    mzh_mlp_recurrent_body<R, false, 2, true>(sm, net, wave, lane, fa, ba, fb, bb, net.dyn0_onehot);
   else
     mzh_mlp_recurrent_body<R, false, 1, true>(sm, net, wave, lane, fa, ba, fb, bb, net.dyn0_onehot);
 }

@@ -106,6 +106,10 @@ struct MzhWMlp {
   const float4* s;  // [17][KB1 + NO][64]
   const float* b1;  // [256]: b1[16ht + 4g + i] = bias1[16ht + 4i + g]
   const float* b2;  // [16 NO]: b2[16ot + 4g + i] = bias2[pi(ot, 4g + i)] (0 on padding rows)
+  // 33-bin heads: bins 0..31 in the NO = 2 tiles, bin 32 as four vector-FMA chains (lane group g: hidden
+  // units 16ht + 4t + g, t = 0..3): w32[4ht + g] = those units' weights, b32 its bias (MzhNet::rwd32)
+  const float4* w32;
+  float b32;
   int kb1, no;
 };
 struct MzhWNet {

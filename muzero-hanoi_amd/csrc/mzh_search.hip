@@ -37,7 +37,7 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
   constexpr int DC = search_dc<R>();
   using Smem = SearchSmem<R, DC>;
   constexpr int RPW = R / 4;  // roots per wave in the tree phases
-  constexpr int N2 = SUP33 ? 3 : 1;
+  constexpr int N2 = SUP33 ? 2 : 1;  // rwd2 / val2 MFMA tiles (bin 32 of a 33-bin head: vector chains)
   extern __shared__ __align__(16) unsigned char smem_raw[];
   MlpSmem<R>& sm = *reinterpret_cast<MlpSmem<R>*>(smem_raw);
   Smem& st = *reinterpret_cast<Smem*>(smem_raw + sizeof(MlpSmem<R>));
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
       // this row's heads (networks.py:83,109,152-189) or its recorded network outputs, in registers
       MzhHeadOut ho;
       if (!REPLAY) {
-        ho = mzh_heads_row<R, SUP33 ? 33 : 0, false>(sm, r, c, net.support, true);
+        ho = mzh_heads_row<R, SUP33 ? 33 : 0, false>(sm, net, r, c, net.support, true);
       } else {
         const float* rec = p.rp_sim + ((size_t)s * p.B + root0 + r) * 8;  // 6 priors, reward, value
         ho.pp = c < MZH_A ? rec[c] : 0.0f;

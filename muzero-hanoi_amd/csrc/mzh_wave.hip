@@ -109,9 +109,11 @@ __device__ __forceinline__ float mzw_add32(float v) {  // rows 0-1 + rows 2-3
 // wave's NT column tiles.  x[n][kb] = the B operand of column tile n, k-block kb (lane group g
 // holds inputs 16kb + 4t + g, t = 0..3).  out[ot][n]: C registers of output tile ot.
 // ------------------------------------------------------------------------------------------
-template <int NT, int KB1, int NO, bool OH>
+// B32 (33-bin heads): also run this lane group's chain of bin 32 (MzhWMlp::w32) on the hidden units it
+// holds, into p32[n]: hidden unit 16ht + 4t + g, ht and t ascending (oracle/mzh_oracle.c linear_head)
+template <int NT, int KB1, int NO, bool OH, bool B32 = false>
 __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[NT][4], const float* const (&oh)[NT],
-                                          floatx4 (&out)[NO][NT], int lane) {
+                                          floatx4 (&out)[NO][NT], int lane, float* p32 = nullptr) {
   constexpr int FR = KB1 + NO;
   const int g = lane >> 4;
   const floatx4* S = reinterpret_cast<const floatx4*>(L.s) + lane;
@@ -127,10 +129,15 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[N
   floatx4 w[FR];
 #pragma unroll
   for (int f = 0; f < FR; ++f) w[f] = S[f * 64];
+  float a32[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) a32[n] = 0.0f;
 #pragma unroll 2
   for (int ht = 0; ht < 16; ++ht) {
     const floatx4* Sn = S + (ht + 1) * FR * 64;  // block 16 is the zero pad
     const floatx4 b = *reinterpret_cast<const floatx4*>(B1 + 16 * ht);
+    floatx4 w32 = {0.f, 0.f, 0.f, 0.f};
+    if (B32) w32 = reinterpret_cast<const floatx4*>(L.w32)[4 * ht + g];
     floatx4 o[NT];
 #pragma unroll
     for (int n = 0; n < NT; ++n)
@@ -160,15 +167,24 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[N
       }
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t) {
 #pragma unroll
       for (int ot = 0; ot < NO; ++ot)
 #pragma unroll
         for (int n = 0; n < NT; ++n)
           out[ot][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[KB1 + ot][t], hid[n][t], out[ot][n], 0, 0, 0);
+      if (B32) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n) a32[n] = __builtin_fmaf(hid[n][t], w32[t], a32[n]);
+      }
+    }
 #pragma unroll
     for (int ot = 0; ot < NO; ++ot) w[KB1 + ot] = Sn[(KB1 + ot) * 64];
     __builtin_amdgcn_sched_barrier(0);
+  }
+  if (B32) {
+#pragma unroll
+    for (int n = 0; n < NT; ++n) p32[n] = a32[n];
   }
 }
 
@@ -217,16 +233,20 @@ __device__ __forceinline__ void mzw_normalize(const floatx4 (&hp)[4][NT], int n,
 // Slot s = 4ot + i of lane group g holds logit k = 2g + (s & 1) + 8(s >> 1) (slot 8 only for g = 0),
 // so the lane's two sequential partials are the oracle's s_{2g}, s_{2g+1} and the cross-group
 // adds reproduce ((s0+s1)+(s2+s3))+((s4+s5)+(s6+s7)).
+// NO = 2: bins 0..31 in the tiles, p32 = this lane group's bin-32 chain (mzw_chain B32), b32 its bias
 template <int NT, int NO>
-__device__ __forceinline__ float mzw_head(const floatx4 (&l)[NO][NT], int n, int lane) {
+__device__ __forceinline__ float mzw_head(const floatx4 (&l)[NO][NT], int n, int lane, float p32 = 0.0f,
+                                          float b32 = 0.0f) {
   const int g = lane >> 4;
   if constexpr (NO == 1) {
     return __shfl(l[0][n][0], lane & 15);  // support 1: the raw logit (networks.py:146-148)
   } else {
+  static_assert(NO == 2, "33-bin heads: two tiles + the bin-32 chains");
   const bool v8 = g == 0;
   float L[9];
 #pragma unroll
-  for (int s = 0; s < 9; ++s) L[s] = l[s >> 2][n][s & 3];
+  for (int s = 0; s < 8; ++s) L[s] = l[s >> 2][n][s & 3];
+  L[8] = mzw_add32(mzw_add16(p32)) + b32;  // ((p0 + p1) + (p2 + p3)) + bias: bin 32 on every group
   float m = L[0];
 #pragma unroll
   for (int s = 1; s < 8; ++s) m = L[s] > m ? L[s] : m;
@@ -367,7 +387,7 @@ __device__ __forceinline__ int mzw_pick_pair(const float (&u)[3], int half, int 
 // simulation then waits for the deepest of 256 roots.
 template <int NT, bool REPLAY, bool SUP33>
 __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net, MzhSearchParams p) {
-  constexpr int NOV = SUP33 ? 3 : 1;
+  constexpr int NOV = SUP33 ? 2 : 1;  // value / reward output tiles (bin 32 of 33: vector chains)
   constexpr int ROOTS = 16 * NT;  // roots per wave
   const float* const noh[NT] = {};  // "no one-hot column" for the chains that take none
   extern __shared__ __align__(16) unsigned char smem_raw[];
@@ -681,10 +701,11 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
     for (int n = 0; n < NT; ++n)
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) hx[n][kb] = hp[kb][n];
-    mzw_chain<NT, 4, NOV, false>(net.rwd, hx, noh, rl, lane);  // reward from h' (networks.py:132-135)
+    float r32[NT], v32[NT];
+    mzw_chain<NT, 4, NOV, false, SUP33>(net.rwd, hx, noh, rl, lane, r32);  // reward from h' (networks.py:132-135)
     mzw_bias2<NT, NOV>(net.rwd, rl, g);
 #pragma unroll
-    for (int n = 0; n < NT; ++n) rew[n] = mzw_head<NT, NOV>(rl, n, lane);
+    for (int n = 0; n < NT; ++n) rew[n] = mzw_head<NT, NOV>(rl, n, lane, SUP33 ? r32[n] : 0.0f, net.rwd.b32);
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
       mzw_normalize<NT>(hp, n, hreg);
@@ -698,10 +719,10 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
     mzw_bias2<NT, 1>(net.pol, pl, g);
 #pragma unroll
     for (int n = 0; n < NT; ++n) cpi[n] = mzw_policy(pl[0][n], lane);
-    mzw_chain<NT, 4, NOV, false>(net.val, hreg, noh, vl, lane);
+    mzw_chain<NT, 4, NOV, false, SUP33>(net.val, hreg, noh, vl, lane, v32);
     mzw_bias2<NT, NOV>(net.val, vl, g);
 #pragma unroll
-    for (int n = 0; n < NT; ++n) val[n] = mzw_head<NT, NOV>(vl, n, lane);
+    for (int n = 0; n < NT; ++n) val[n] = mzw_head<NT, NOV>(vl, n, lane, SUP33 ? v32[n] : 0.0f, net.val.b32);
   };
 
   // the new node's block, then backup (node.py:30-70)

@@ -260,6 +260,27 @@ static void linear(const float* x, int K, const float* W, const float* b, int N,
   }
 }
 
+/* The value / reward output layer (33 support bins): bins 0..31 as `linear` (the GPU's MFMA tiles),
+ * bin 32 -- the one logit past two 16-row tiles -- as four k-ordered fmaf chains over k = g, g + 4,
+ * g + 8, ... (g = 0..3) combined ((p0 + p1) + (p2 + p3)), bias after: the order the GPU kernels
+ * compute it in with vector FMAs instead of a third, 15/16-padding MFMA tile (muzero-hanoi_amd/csrc,
+ * MzhWMlp::w32) */
+static void linear_head(const float* x, const float* W, const float* b, int N, float* y) {
+  if (N != ORC_MAXSUP) {
+    linear(x, ORC_F, W, b, N, y, 0);
+    return;
+  }
+  linear(x, ORC_F, W, b, N - 1, y, 0);
+  const float* wr = W + (size_t)(N - 1) * ORC_F;
+  float p[4];
+  for (int g = 0; g < 4; ++g) {
+    float acc = 0.0f;
+    for (int k = g; k < ORC_F; k += 4) acc = fmaf(x[k], wr[k], acc);
+    p[g] = acc;
+  }
+  y[N - 1] = ((p[0] + p[1]) + (p[2] + p[3])) + b[N - 1];
+}
+
 typedef struct {
   float h[ORC_H];
   float reward;
@@ -276,7 +297,7 @@ static void prediction(const orc_weights* w, const float* h, orc_netout* o) {
   linear(h, ORC_H, w->pol0_w, w->pol0_b, ORC_F, hid, 1);
   linear(hid, ORC_F, w->pol2_w, w->pol2_b, ORC_A, o->policy_logits, 0);
   linear(h, ORC_H, w->val0_w, w->val0_b, ORC_F, hid, 1);
-  linear(hid, ORC_F, w->val2_w, w->val2_b, w->support, o->value_logits, 0);
+  linear_head(hid, w->val2_w, w->val2_b, w->support, o->value_logits);
   o->value = orc_logits_to_value(o->value_logits, w->support);
   softmax(o->policy_logits, ORC_A, o->pi);
 }
@@ -302,7 +323,7 @@ static void recurrent_inference(const orc_weights* w, const float* h_in, int act
   linear(x, ORC_H + ORC_A, w->dyn0_w, w->dyn0_b, ORC_F, hid, 1);
   linear(hid, ORC_F, w->dyn2_w, w->dyn2_b, ORC_H, o->h, 0);
   linear(o->h, ORC_H, w->rwd0_w, w->rwd0_b, ORC_F, hid, 1);
-  linear(hid, ORC_F, w->rwd2_w, w->rwd2_b, w->support, o->reward_logits, 0);
+  linear_head(hid, w->rwd2_w, w->rwd2_b, w->support, o->reward_logits);
   o->reward = orc_logits_to_value(o->reward_logits, w->support);
   normalize_h(o->h);
   prediction(w, o->h, o);
