@@ -335,6 +335,7 @@ struct MlpSmem {
   float lpol[R * MZH_LDPOL];  // policy logits
   float lval[R * MZH_LDSUP];  // value logits
   float lrwd[R * MZH_LDSUP];  // reward logits
+  float w32[2 * 256];         // bin 32 of the 33-bin reward / value heads: rwd32 | val32 packing (mzh_w32_fill)
   float pi[R * 8];
   float value[R];
   float reward[R];
@@ -721,14 +722,15 @@ __device__ __forceinline__ void mzh_normalize_par(const float* src, float* dst, 
 struct MzhHeadOut {
   float pp, value, reward;
 };
-template <int R, int SUP = 0, bool STORE = true, class SM>
+// CHAIN32 = false: bin 32 of a 33-bin head is already in lval / lrwd (mzh_bin32_wave ran in the MLP).
+template <int R, int SUP = 0, bool STORE = true, bool CHAIN32 = true, class SM>
 __device__ __forceinline__ MzhHeadOut mzh_heads_row(SM& sm, const MzhNet& net, int row, int q, int support_in,
                                                    bool recurrent) {
   const int support = SUP ? SUP : support_in;
   // bin 32 of the reward (lanes 0-3) and value (lanes 4-7) logits: lane c of the quad runs chain c over
   // hidden units 16b + 4j + c -- LDS positions 16b + 4c + j (k-block order), one ds_read_b128 per block
   float l32r = 0.0f, l32v = 0.0f;
-  if (support == 33) {
+  if (CHAIN32 && support == 33) {
     const int hv = q >> 2, c = q & 3;
     const float* hid = (hv ? sm.hidV : sm.hidR) + row * MZH_LD256 + 4 * c;
     const float4* w = (hv ? net.val32 : net.rwd32) + c;
@@ -773,7 +775,7 @@ __device__ __forceinline__ MzhHeadOut mzh_heads_row(SM& sm, const MzhNet& net, i
     for (int i = 0; i < 5; ++i) {
       const int k = q + 8 * i;
       // bin 32 (lane 0, i = 4) from the vector chains above
-      const float raw = i == 4 ? (h ? l32r : l32v) : lv[h][k];
+      const float raw = (CHAIN32 && i == 4) ? (h ? l32r : l32v) : lv[h][k];
       e[h][i] = (h < nh && k < 33) ? raw : -__builtin_inff();
       m[h] = e[h][i] > m[h] ? e[h][i] : m[h];
     }
@@ -863,10 +865,56 @@ __device__ __forceinline__ MzhHeadOut mzh_heads_row(SM& sm, const MzhNet& net, i
 }
 
 // all rows: 8 lanes per row, row = tid / 8 (32 rows over 256 threads)
-template <int R, class SM>
+template <int R, bool CHAIN32 = true, class SM>
 __device__ __forceinline__ void mzh_heads_par(SM& sm, const MzhNet& net, bool recurrent, int tid) {
   const int row = tid >> 3, q = tid & 7;
-  if (row < R) mzh_heads_row<R>(sm, net, row, q, net.support, recurrent);
+  if (row < R) mzh_heads_row<R, 0, true, CHAIN32>(sm, net, row, q, net.support, recurrent);
+}
+
+// LDS copy of the bin-32 weight rows (rwd32, val32) for mzh_bin32_wave; before a barrier
+template <int R, class SM>
+__device__ __forceinline__ void mzh_w32_fill(SM& sm, const MzhNet& net, int tid) {
+  if (tid < 128) reinterpret_cast<float4*>(sm.w32)[tid] = tid < 64 ? net.rwd32[tid] : net.val32[tid - 64];
+}
+
+// Bin 32 of the 33-bin reward and value logits of all R rows on ONE wave -- the wave without a
+// pol2 / val2 tile in the last MLP phase, whose slot is otherwise idle.  Chain c of oracle
+// linear_head runs over hidden units 16b + 4j + c, at LDS positions 16b + 4c + j; the result is
+// ((p0 + p1) + (p2 + p3)) + bias, stored to column 32 of lrwd / lval (the heads then read it like
+// bins 0-31).  R = 32: lane -> (row, head), four chains per lane.  R = 16: lane -> (row, head,
+// chain pair), the pairs' sums exchanged across the half-waves.  Weights come from the LDS copy
+// (two distinct addresses per read: a broadcast).
+template <int R, class SM>
+__device__ __forceinline__ void mzh_bin32_wave(SM& sm, const MzhNet& net, int lane) {
+  static_assert(R == 16 || R == 32, "rows per workgroup");
+  constexpr int CH = R == 32 ? 4 : 2;  // chains per lane
+  const int row = lane & (R - 1);
+  const bool hv = (lane / R) & 1;  // value head / reward head
+  const int c0 = R == 32 ? 0 : 2 * (lane >> 5);
+  const float* hid = (hv ? sm.hidV : sm.hidR) + row * MZH_LD256 + 4 * c0;
+  const floatx4* w = reinterpret_cast<const floatx4*>(sm.w32 + (hv ? 256 : 0)) + c0;
+  float acc[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) acc[c] = 0.0f;
+#pragma unroll
+  for (int b = 0; b < 16; ++b)
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const floatx4 a4 = *reinterpret_cast<const floatx4*>(hid + 16 * b + 4 * c);
+      const floatx4 w4 = w[4 * b + c];
+      acc[c] = __builtin_fmaf(a4[0], w4[0], acc[c]);
+      acc[c] = __builtin_fmaf(a4[1], w4[1], acc[c]);
+      acc[c] = __builtin_fmaf(a4[2], w4[2], acc[c]);
+      acc[c] = __builtin_fmaf(a4[3], w4[3], acc[c]);
+    }
+  const float p = acc[0] + acc[1];
+  float l32;
+  if constexpr (R == 32)
+    l32 = p + (acc[2] + acc[3]);
+  else
+    l32 = p + __shfl_xor(p, 32);
+  l32 = l32 + (hv ? net.val32b : net.rwd32b);
+  if (R == 32 || lane < 32) (hv ? sm.lval : sm.lrwd)[row * MZH_LDSUP + 32] = l32;
 }
 
 // The per-wave chunk schedule of the prediction function (networks.py:140-150) on sm.x:
@@ -882,9 +930,10 @@ __device__ __forceinline__ MzhChunk mzh_head_chunk(SM& sm, const MzhNet& net, in
   if (wave == 0) return mzh_chunk(net.pol2, 0, 1, sm.lpol, MZH_LDPOL);
   return mzh_chunk(net.val2, wave - 1 < net.val2.nt ? wave - 1 : 0, wave - 1 < net.val2.nt ? 1 : 0, sm.lval, MZH_LDSUP);
 }
-// waves with a pol2 / val2 tile: all four for 33-bin heads (N2 = 3), waves 0-1 for scalar heads
+// waves with a pol2 / val2 tile: 0-2 for 33-bin heads (N2 = 2; wave 3 runs bin 32 by vector chains),
+// 0-1 for scalar heads
 template <int N2>
-__device__ __forceinline__ bool mzh_has_head_tile(int wave) { return N2 == 3 || wave <= N2; }  // compile-time for N2 = 3
+__device__ __forceinline__ bool mzh_has_head_tile(int wave) { return wave <= N2; }
 
 // nj consecutive tiles of the prediction hidden layers' 32-tile strip (tiles 0-15: pol0 -> hidP,
 // 16-31: val0 -> hidV; both read the normalised latent), starting at strip tile t0
@@ -958,7 +1007,7 @@ __device__ __forceinline__ void mzh_mlp_fetch12(SM& sm, const MzhNet& net, int w
   mzh_fetch<1, 16, true>(fb, bb, mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64), lane);
 }
 
-// N2 = reward / value layer-2 tiles (3: 33-bin support, 1: scalar); HEADS: finish with the heads on
+// N2 = reward / value layer-2 tiles (2: 33-bin support, bins 0-31; 1: scalar); HEADS: finish with the heads on
 // all rows (standalone inference) -- the search kernel runs each root's heads itself.
 template <int R, bool NEXT, int N2, bool HEADS, class SM, class BAR = MzhSyncBar>
 __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net, int wave_in, int lane,
@@ -1054,14 +1103,15 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
                                                     &c_n1);  // pol2 / val2
       else
         mzh_mma_store<MT, 1, 16, true, 0, 0, true>(fa, ba, c_h, hin, MZH_LD256, false, nullptr, nullptr, lane);
-    } else if (NEXT) {
-      mzh_fetch<4, 4, true>(fa, ba, c_n1, lane);  // next step's dyn0 chunk
+    } else {
+      if (NEXT) mzh_fetch<4, 4, true>(fa, ba, c_n1, lane);  // next step's dyn0 chunk
+      if (N2 == 2) mzh_bin32_wave<R>(sm, net, lane);      // 33-bin heads: wave 3 (no head tile) runs bin 32
     }
   }
   MZH_STAMP(10);
   bar();
   if (HEADS) {
-    mzh_heads_par<R>(sm, net, true, tid);
+    mzh_heads_par<R, N2 != 2>(sm, net, true, tid);
     MZH_STAMP(11);
     bar();
   }
@@ -1073,6 +1123,10 @@ __device__ void mzh_mlp_recurrent(MlpSmem<R>& sm, const MzhNet& net, int wave, i
   floatx4 fa[16], fb[16];
   float ba[4], bb[4];
   mzh_mlp_fetch12<R>(sm, net, wave, lane, fa, ba, fb, bb);
+  if (net.support == 33) {
+    mzh_w32_fill<R>(sm, net, threadIdx.x);
+    __syncthreads();
+  }
   if (net.support == 33)
     mzh_mlp_recurrent_body<R, false, 2, true>(sm, net, wave, lane, fa, ba, fb, bb, net.dyn0_onehot);
   else

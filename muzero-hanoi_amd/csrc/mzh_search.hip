@@ -60,6 +60,7 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
 
   if (OHL)
     for (int i = tid; i < MZH_A * MZH_F; i += MZH_THREADS) ohl[i] = net.dyn0_onehot[i];
+  if (SUP33 && !REPLAY) mzh_w32_fill<R>(sm, net, tid);
   for (int i = tid; i < S + 3; i += MZH_THREADS) {
     table[i] = i < S + 2 ? p.table[i] : 0.0;
     inv[i] = 1.0 / (double)i;  // IEEE division: correctly rounded
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
       // this row's heads (networks.py:83,109,152-189) or its recorded network outputs, in registers
       MzhHeadOut ho;
       if (!REPLAY) {
-        ho = mzh_heads_row<R, SUP33 ? 33 : 0, false>(sm, net, r, c, net.support, true);
+        ho = mzh_heads_row<R, SUP33 ? 33 : 0, false, !SUP33>(sm, net, r, c, net.support, true);
       } else {
         const float* rec = p.rp_sim + ((size_t)s * p.B + root0 + r) * 8;  // 6 priors, reward, value
         ho.pp = c < MZH_A ? rec[c] : 0.0f;
