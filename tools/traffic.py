@@ -26,13 +26,26 @@ def kind(name):
     return "tree" if args[1].strip() == "true" else "fused"
 
 
-def summarise(root, tag):
-    out = {"fused": {}, "tree": {}}
+def summarise(root, tag, want=None):
+    """want: {"fused": name, "tree": name} -- the instantiations the bench line reports; any other
+    search-kernel instantiation the command launched (e.g. the minmax_in leg's MMIN = true) is listed
+    under "other" with its stats and kept out of the fused / tree figures"""
+    out = {"fused": {}, "tree": {}, "other": {}}
+    want = want or {}
+
+    def slot(name):
+        k = kind(name)
+        if k and want.get(k) and want[k] not in name:
+            return "other"
+        return k
+
     ks = newest(root, f"prof_{tag}_trace/*/*_kernel_stats.csv") or newest(root, f"prof_{tag}_trace/*_kernel_stats.csv")
     if ks:
         for r in csv.DictReader(open(ks)):
-            k = kind(r["Name"])
-            if k:
+            k = slot(r["Name"])
+            if k == "other":
+                out["other"][r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
+            elif k:
                 out[k].update(kernel=r["Name"], calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]))
     for p in ("hit", "fetch", "write", "sq"):
         f = newest(root, f"prof_{tag}_{p}/*/*_counter_collection.csv") or newest(root, f"prof_{tag}_{p}/*_counter_collection.csv")
@@ -41,13 +54,15 @@ def summarise(root, tag):
         agg = {"fused": collections.defaultdict(lambda: collections.defaultdict(float)),
                "tree": collections.defaultdict(lambda: collections.defaultdict(float))}
         for r in csv.DictReader(open(f)):
-            k = kind(r["Kernel_Name"])
-            if k:  # sum the per-XCD / per-SE rows of one dispatch
+            k = slot(r["Kernel_Name"])
+            if k in agg:  # sum the per-XCD / per-SE rows of one dispatch
                 agg[k][r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
         for k in agg:
             for c, per in agg[k].items():
                 out[k][c] = sum(per.values()) / len(per)  # mean over dispatches
     for k, d in out.items():
+        if k == "other":
+            continue
         if "TCC_HIT_sum" in d:
             d["l2_hit_rate"] = d["TCC_HIT_sum"] / (d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
         if "FETCH_SIZE" in d:
@@ -95,9 +110,13 @@ def main():
     ap.add_argument("--expect-build", default=None,
                     help="build id the profiled run must report (default: the checked-out sources' hash)")
     a = ap.parse_args()
-    out = summarise(a.root, a.tag)
     prof = bench_line(os.path.join(a.root, f"prof_{a.tag}_trace.log"))
     plain = bench_line(os.path.join(a.root, f"prof_{a.tag}_plain.json"))
+    ref = prof or plain
+    want = None
+    if ref is not None:
+        want = {"fused": ref["roofline"]["kernel"], "tree": (ref["roofline"].get("tree") or {}).get("kernel")}
+    out = summarise(a.root, a.tag, want)
     if plain is not None:
         r = plain["roofline"]
         out["unprofiled"] = {
