@@ -69,7 +69,8 @@ def build(verbose=False, force=False, diag=False, tag="", defines=()):
     sfx = ("_diag" if diag else "") + (f"_{tag}" if tag else "")
     obj_dir = OBJ + sfx
     lib_path = LIB.replace("libmzh.so", f"libmzh{sfx}.so")
-    flags = FLAGS + (["-DMZH_STAMPS"] if diag else []) + [f"-D{d}" for d in defines]
+    # a define list entry starting with '-' is a compiler flag (e.g. -fno-slp-vectorize), else -D<entry>
+    flags = FLAGS + (["-DMZH_STAMPS"] if diag else []) + [d if d.startswith("-") else f"-D{d}" for d in defines]
     os.makedirs(obj_dir, exist_ok=True)
     # the objects of a variant directory are only reusable for the same flags: a stamp file records
     # them, and a change forces a rebuild (A/B builds of one tag with different -D lists)
