@@ -111,13 +111,23 @@ __device__ __forceinline__ float mzw_add32(float v) {  // rows 0-1 + rows 2-3
 // ------------------------------------------------------------------------------------------
 // B32 (33-bin heads): also run this lane group's chain of bin 32 (MzhWMlp::w32) on the hidden units it
 // holds, into p32[n]: hidden unit 16ht + 4t + g, ht and t ascending (oracle/mzh_oracle.c linear_head)
+// The weight stream goes through a buffer resource: the lane's byte offset sits in one VGPR, the
+// fragment / block offset is uniform (SGPR or immediate), so no load costs 64-bit VALU address
+// arithmetic (the 64-bit pointer form spent ~13 VALU per two hidden blocks on it).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mzw_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ floatx4 mzw_ld4(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
 template <int NT, int KB1, int NO, bool OH, bool B32 = false>
 __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[NT][4], const float* const (&oh)[NT],
                                           floatx4 (&out)[NO][NT], int lane, float* p32 = nullptr) {
   constexpr int FR = KB1 + NO;
   const int g = lane >> 4;
-  const floatx4* S = reinterpret_cast<const floatx4*>(L.s) + lane;
-  const float* B1 = L.b1 + 4 * g;
+  const __amdgpu_buffer_rsrc_t rs = mzw_rsrc(L.s), rb = mzw_rsrc(L.b1), r32 = mzw_rsrc(L.w32);
+  const int vs = 16 * lane, vb = 16 * g;  // byte offsets: the lane's fragment slot, its group's 4 biases
 #pragma unroll
   for (int ot = 0; ot < NO; ++ot)
 #pragma unroll
@@ -128,16 +138,16 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[N
   // the compiler from sinking the refills to their uses.
   floatx4 w[FR];
 #pragma unroll
-  for (int f = 0; f < FR; ++f) w[f] = S[f * 64];
+  for (int f = 0; f < FR; ++f) w[f] = mzw_ld4(rs, vs, f * 1024);
   float a32[NT];
 #pragma unroll
   for (int n = 0; n < NT; ++n) a32[n] = 0.0f;
 #pragma unroll 2
   for (int ht = 0; ht < 16; ++ht) {
-    const floatx4* Sn = S + (ht + 1) * FR * 64;  // block 16 is the zero pad
-    const floatx4 b = *reinterpret_cast<const floatx4*>(B1 + 16 * ht);
+    const int sn = (ht + 1) * FR * 1024;  // next block's byte offset (block 16 is the zero pad)
+    const floatx4 b = mzw_ld4(rb, vb, 64 * ht);
     floatx4 w32 = {0.f, 0.f, 0.f, 0.f};
-    if (B32) w32 = reinterpret_cast<const floatx4*>(L.w32)[4 * ht + g];
+    if (B32) w32 = mzw_ld4(r32, vb, 64 * ht);
     floatx4 o[NT];
 #pragma unroll
     for (int n = 0; n < NT; ++n)
@@ -152,7 +162,7 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[N
 #pragma unroll
         for (int n = 0; n < NT; ++n)
           acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[kb][t], x[n][kb][t], acc[n], 0, 0, 0);
-      w[kb] = Sn[kb * 64];
+      w[kb] = mzw_ld4(rs, vs, sn + kb * 1024);
       __builtin_amdgcn_sched_barrier(0);
     }
     floatx4 hid[NT];
@@ -179,7 +189,7 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[N
       }
     }
 #pragma unroll
-    for (int ot = 0; ot < NO; ++ot) w[KB1 + ot] = Sn[(KB1 + ot) * 64];
+    for (int ot = 0; ot < NO; ++ot) w[KB1 + ot] = mzw_ld4(rs, vs, sn + (KB1 + ot) * 1024);
     __builtin_amdgcn_sched_barrier(0);
   }
   if (B32) {
