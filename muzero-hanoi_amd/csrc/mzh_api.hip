@@ -328,9 +328,12 @@ extern "C" int mzh_load_weights(mzh_engine* eng, const float* flat, size_t n_flo
     m.b = base + pl.boff;
     m.kb = pl.kb;
     m.nt = pl.nt;
+    m.woff = (int)(pl.woff * sizeof(float));
+    m.boff = (int)(pl.boff * sizeof(float));
     return m;
   };
   MzhNet& n = eng->net;
+  n.wbase = base;
   n.rep0 = mk(L[0]); n.rep2 = mk(L[1]); n.dyn0 = mk(L[2]); n.dyn2 = mk(L[3]); n.rwd0 = mk(L[4]);
   n.rwd2 = mk(L[5]); n.pol0 = mk(L[6]); n.pol2 = mk(L[7]); n.val0 = mk(L[8]); n.val2 = mk(L[9]);
   if (n.val0.w != n.pol0.w + (size_t)n.pol0.nt * n.pol0.kb * 64)
@@ -355,9 +358,14 @@ extern "C" int mzh_load_weights(mzh_engine* eng, const float* flat, size_t n_flo
     m.no = pw.no;
     m.w32 = pw.w32off ? reinterpret_cast<const float4*>(base + pw.w32off) : nullptr;
     m.b32 = pw.b32;
+    m.soff = (int)(pw.soff * sizeof(float));
+    m.b1off = (int)(pw.b1off * sizeof(float));
+    m.b2off = (int)(pw.b2off * sizeof(float));
+    m.w32off = (int)(pw.w32off * sizeof(float));
     return m;
   };
   MzhWNet& w = eng->wnet;
+  w.wbase = base;
   w.rep = mkw(WL[0]); w.dyn = mkw(WL[1]); w.rwd = mkw(WL[2]); w.pol = mkw(WL[3]); w.val = mkw(WL[4]);
   w.oh = base + wohoff;
   w.support = sup;

@@ -294,6 +294,7 @@ struct MzhLayer {
   const float4* w;  // [NT][KB][64]
   const float* b;   // [16*NT]
   int kb, nt;
+  int woff, boff;  // byte offsets of w and b in the packed weight blob (MzhNet::wbase)
 };
 
 // Support 33: rwd2 / val2 hold bins 0..31 (two 16-row tiles); bin 32 -- which would cost a third
@@ -303,6 +304,7 @@ struct MzhLayer {
 // W[32][16b + 12 + g]}: the weights of chain g in its order (shared with the wave kernel, MzhWMlp::w32)
 struct MzhNet {
   MzhLayer rep0, rep2, dyn0, dyn2, rwd0, rwd2, pol0, pol2, val0, val2;
+  const float* wbase;  // the packed weight blob every layer lives in (one buffer resource for all chunks)
   const float* dyn0_onehot;  // [6][256]: dynamic_net.0.weight[:, 64 + a]
   const float4 *rwd32, *val32;
   float rwd32b, val32b;
@@ -435,23 +437,39 @@ struct MzhSyncBar {
   __device__ __forceinline__ void operator()() const { __syncthreads(); }
 };
 
+// Weight chunks address the packed blob through one buffer resource: a tile is a uniform byte
+// offset (one SGPR instead of a 64-bit pointer), the lane's slot a VGPR offset, so no load costs
+// VALU address arithmetic.
 struct MzhChunk {
-  const float4* w[4];
-  const float* bias[4];  // already offset to the tile's first column
-  float* out[4];         // LDS output base per tile (a chunk may span two layers sharing A)
+  const float* wbase;  // the packed weight blob
+  int woff[4];         // byte offset of each tile's fragments
+  int boff[4];         // byte offset of each tile's first bias
+  float* out[4];       // LDS output base per tile (a chunk may span two layers sharing A)
   int col0[4];
-  int ldo, nj;           // nj: active tiles (wave-uniform), <= NJ
+  int ldo, nj;         // nj: active tiles (wave-uniform), <= NJ
 };
 
-__device__ __forceinline__ MzhChunk mzh_chunk(const MzhLayer& L, int nt0, int nj, float* out, int ldo) {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mzh_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ floatx4 mzh_ld4(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ float mzh_ld1(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
+__device__ __forceinline__ MzhChunk mzh_chunk(const MzhNet& net, const MzhLayer& L, int nt0, int nj, float* out,
+                                              int ldo) {
   MzhChunk c;
   c.ldo = ldo;
   c.nj = nj;
+  c.wbase = net.wbase;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int nt = nt0 + (q < nj ? q : 0);
-    c.w[q] = L.w + (size_t)nt * L.kb * 64;
-    c.bias[q] = L.b + nt * 16;
+    c.woff[q] = L.woff + nt * L.kb * 1024;
+    c.boff[q] = L.boff + nt * 64;
     c.col0[q] = nt * 16;
     c.out[q] = out;
   }
@@ -463,19 +481,17 @@ __device__ __forceinline__ MzhChunk mzh_chunk(const MzhLayer& L, int nt0, int nj
 template <int NJ, int KB, bool ALL = false>
 __device__ __forceinline__ void mzh_fetch(floatx4* f, float* bv, const MzhChunk& c, int lane) {
   static_assert(NJ * KB <= 16, "chunk too large");
+  const __amdgpu_buffer_rsrc_t rs = mzh_rsrc(c.wbase);
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
 #pragma unroll
     for (int q = 0; q < NJ; ++q) {
-      if (ALL || q < c.nj) {
-        const float4 t = c.w[q][kb * 64 + lane];
-        f[q * KB + kb] = floatx4{t.x, t.y, t.z, t.w};
-      }
+      if (ALL || q < c.nj) f[q * KB + kb] = mzh_ld4(rs, 16 * lane, c.woff[q] + kb * 1024);
     }
   }
 #pragma unroll
   for (int q = 0; q < NJ; ++q)
-    if (ALL || q < c.nj) bv[q] = c.bias[q][lane & 15];
+    if (ALL || q < c.nj) bv[q] = mzh_ld1(rs, 4 * (lane & 15), c.boff[q]);
 }
 
 // acc = A[rows][0:16KB] . W-tiles ; epilogue (+onehot) + bias (+relu) -> LDS
@@ -506,11 +522,9 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
   // of one phase that share A load it once)
   static_assert(PT <= 16 && PNB <= 4, "ring chunk too large");
   const int r = lane & 15, g = lane >> 4;
-  const float4* pw = PT > 0 ? pc->w[0] : nullptr;
-  auto refill = [&](int slot) {
-    const float4 t = pw[slot * 64 + lane];
-    f[slot] = floatx4{t.x, t.y, t.z, t.w};
-  };
+  const __amdgpu_buffer_rsrc_t prs = mzh_rsrc(PT > 0 ? pc->wbase : c.wbase);
+  const int pw = PT > 0 ? pc->woff[0] : 0;
+  auto refill = [&](int slot) { f[slot] = mzh_ld4(prs, 16 * lane, pw + slot * 1024); };
   auto fs = [](int q, int kb) { return q * KB + kb; };
 #pragma unroll
   for (int slot = NJ * KB; slot < PT; ++slot) refill(slot);
@@ -609,7 +623,7 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
     }
   }
 #pragma unroll
-  for (int q = 0; q < PNB; ++q) bv[q] = pc->bias[q][lane & 15];
+  for (int q = 0; q < PNB; ++q) bv[q] = mzh_ld1(prs, 4 * (lane & 15), pc->boff[q]);
 }
 
 // normalize_h_state (networks.py:191-196): 8 lanes per row, 8 elements per lane.
@@ -922,13 +936,13 @@ __device__ __forceinline__ void mzh_bin32_wave(SM& sm, const MzhNet& net, int la
 template <int R, class SM>
 __device__ __forceinline__ MzhChunk mzh_pred_chunk(SM& sm, const MzhNet& net, int wave, int c) {
   const int id0 = wave * 8 + c * 4;
-  return id0 >= 16 ? mzh_chunk(net.val0, id0 - 16, 4, sm.hidV, MZH_LD256)
-                   : mzh_chunk(net.pol0, id0, 4, sm.hidP, MZH_LD256);
+  return id0 >= 16 ? mzh_chunk(net, net.val0, id0 - 16, 4, sm.hidV, MZH_LD256)
+                   : mzh_chunk(net, net.pol0, id0, 4, sm.hidP, MZH_LD256);
 }
 template <int R, class SM>
 __device__ __forceinline__ MzhChunk mzh_head_chunk(SM& sm, const MzhNet& net, int wave) {
-  if (wave == 0) return mzh_chunk(net.pol2, 0, 1, sm.lpol, MZH_LDPOL);
-  return mzh_chunk(net.val2, wave - 1 < net.val2.nt ? wave - 1 : 0, wave - 1 < net.val2.nt ? 1 : 0, sm.lval, MZH_LDSUP);
+  if (wave == 0) return mzh_chunk(net, net.pol2, 0, 1, sm.lpol, MZH_LDPOL);
+  return mzh_chunk(net, net.val2, wave - 1 < net.val2.nt ? wave - 1 : 0, wave - 1 < net.val2.nt ? 1 : 0, sm.lval, MZH_LDSUP);
 }
 // waves with a pol2 / val2 tile: 0-2 for 33-bin heads (N2 = 2; wave 3 runs bin 32 by vector chains),
 // 0-1 for scalar heads
@@ -942,14 +956,15 @@ __device__ __forceinline__ MzhChunk mzh_pred_tiles(SM& sm, const MzhNet& net, in
   MzhChunk c;
   c.ldo = MZH_LD256;
   c.nj = nj;
+  c.wbase = net.wbase;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int t = t0 + (q < nj ? q : 0);
     const bool v = t >= 16;
     const MzhLayer& L = v ? net.val0 : net.pol0;
     const int nt = t & 15;
-    c.w[q] = L.w + (size_t)nt * L.kb * 64;
-    c.bias[q] = L.b + nt * 16;
+    c.woff[q] = L.woff + nt * L.kb * 1024;
+    c.boff[q] = L.boff + nt * 64;
     c.col0[q] = nt * 16;
     c.out[q] = v ? sm.hidV : sm.hidP;
   }
@@ -1003,8 +1018,8 @@ template <int R, class SM>
 __device__ __forceinline__ void mzh_mlp_fetch12(SM& sm, const MzhNet& net, int wave_in, int lane, floatx4* fa,
                                                 float* ba, floatx4* fb, float* bb) {
   const int wave = __builtin_amdgcn_readfirstlane(wave_in);
-  mzh_fetch<4, 4, true>(fa, ba, mzh_chunk(net.dyn0, wave * 4, 4, sm.hidP, MZH_LD256), lane);
-  mzh_fetch<1, 16, true>(fb, bb, mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64), lane);
+  mzh_fetch<4, 4, true>(fa, ba, mzh_chunk(net, net.dyn0, wave * 4, 4, sm.hidP, MZH_LD256), lane);
+  mzh_fetch<1, 16, true>(fb, bb, mzh_chunk(net, net.dyn2, wave, 1, sm.hraw, MZH_LD64), lane);
 }
 
 // N2 = reward / value layer-2 tiles (2: 33-bin support, bins 0-31; 1: scalar); HEADS: finish with the heads on
@@ -1026,18 +1041,18 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
   const int P1 = r2 ? wave * (N2 + 4) : N2 * (N2 + 4) + (wave - N2) * (N2 + 8);
   const int P2 = P1 + (r2 ? 0 : 4), P3 = P2 + 4;
   const bool ht = mzh_has_head_tile<N2>(wave);
-  const MzhChunk c_rwd0 = mzh_chunk(net.rwd0, wave * 4, 4, sm.hidR, MZH_LD256);
+  const MzhChunk c_rwd0 = mzh_chunk(net, net.rwd0, wave * 4, 4, sm.hidR, MZH_LD256);
   const MzhChunk c_p2 = mzh_pred_tiles<R>(sm, net, P2, 4);
   MZH_STAMP_DECL
   MZH_STAMP(0);
-  mzh_mma_store<MT, 4, 4, true, 16, 4>(fa, ba, mzh_chunk(net.dyn0, wave * 4, 4, sm.hidP, MZH_LD256), sm.x, MZH_LD64,
+  mzh_mma_store<MT, 4, 4, true, 16, 4>(fa, ba, mzh_chunk(net, net.dyn0, wave * 4, 4, sm.hidP, MZH_LD256), sm.x, MZH_LD64,
                                        true, onehot, sm.act, lane, &c_rwd0);  // dyn0 + one-hot + bias, relu
   MZH_STAMP(1);
   bar();
   MZH_STAMP(2);
   {
-    const MzhChunk c_b = r2 ? mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP) : mzh_pred_tiles<R>(sm, net, P1, 4);
-    mzh_mma_store<MT, 1, 16, true, 16, 4>(fb, bb, mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64), sm.hidP, MZH_LD256,
+    const MzhChunk c_b = r2 ? mzh_chunk(net, net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP) : mzh_pred_tiles<R>(sm, net, P1, 4);
+    mzh_mma_store<MT, 1, 16, true, 16, 4>(fb, bb, mzh_chunk(net, net.dyn2, wave, 1, sm.hraw, MZH_LD64), sm.hidP, MZH_LD256,
                                           false, nullptr, nullptr, lane, &c_b);  // dyn2 -> h'
   }
   MZH_STAMP(3);
@@ -1071,7 +1086,7 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
     }
     const MzhChunk c_p3 = mzh_pred_tiles<R>(sm, net, P3, N2);
     if (r2)
-      mzh_mma_store<MT, 1, 16, true, 4 * N2, N2, true>(fb, bb, mzh_chunk(net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP),
+      mzh_mma_store<MT, 1, 16, true, 4 * N2, N2, true>(fb, bb, mzh_chunk(net, net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP),
                                                        sm.hidR, MZH_LD256, false, nullptr, nullptr, lane,
                                                        &c_p3);  // rwd2 -> reward logits
     else
@@ -1085,7 +1100,7 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
       mzh_mma_store<MT, 4, 4, true>(fa, ba, c_p2, sm.x, MZH_LD64, true, nullptr, nullptr, lane, nullptr, ax);
     }
     if (NEXT) {
-      const MzhChunk c_n2 = mzh_chunk(net.dyn2, wave, 1, sm.hraw, MZH_LD64);
+      const MzhChunk c_n2 = mzh_chunk(net, net.dyn2, wave, 1, sm.hraw, MZH_LD64);
       mzh_mma_store<MT, N2, 4, true, 16, 1>(fb, bb, c_p3, sm.x, MZH_LD64, true, nullptr, nullptr, lane, &c_n2, ax);
     } else {
       mzh_mma_store<MT, N2, 4, true>(fb, bb, c_p3, sm.x, MZH_LD64, true, nullptr, nullptr, lane, nullptr, ax);
@@ -1094,7 +1109,7 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
   MZH_STAMP(9);
   bar();
   {
-    const MzhChunk c_n1 = mzh_chunk(net.dyn0, wave * 4, 4, sm.hidP, MZH_LD256);
+    const MzhChunk c_n1 = mzh_chunk(net, net.dyn0, wave * 4, 4, sm.hidP, MZH_LD256);
     if (ht) {
       const MzhChunk c_h = mzh_head_chunk<R>(sm, net, wave);
       float* hin = wave == 0 ? sm.hidP : sm.hidV;

@@ -111,9 +111,11 @@ struct MzhWMlp {
   const float4* w32;
   float b32;
   int kb1, no;
+  int soff, b1off, b2off, w32off;  // byte offsets of s, b1, b2, w32 in the packed blob (MzhWNet::wbase)
 };
 struct MzhWNet {
   MzhWMlp rep, dyn, rwd, pol, val;
+  const float* wbase;  // the packed weight blob: one buffer resource serves every chain's loads
   const float* oh;  // [6][256]: oh[a][16ht + 4g + i] = dynamic_net.0.weight[u(ht, 4g + i)][64 + a]
   int support, in_dim;
 };

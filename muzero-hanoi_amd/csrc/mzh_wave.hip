@@ -121,12 +121,13 @@ __device__ __forceinline__ floatx4 mzw_ld4(__amdgpu_buffer_rsrc_t r, int voff, i
   return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
+// rw: the blob's buffer resource (MzhWNet::wbase, made once per kernel: one SGPR quad for every chain)
 template <int NT, int KB1, int NO, bool OH, bool B32 = false>
-__device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[NT][4], const float* const (&oh)[NT],
-                                          floatx4 (&out)[NO][NT], int lane, float* p32 = nullptr) {
+__device__ __forceinline__ void mzw_chain(const MzhWMlp& L, __amdgpu_buffer_rsrc_t rw, const floatx4 (&x)[NT][4],
+                                          const float* const (&oh)[NT], floatx4 (&out)[NO][NT], int lane,
+                                          float* p32 = nullptr) {
   constexpr int FR = KB1 + NO;
   const int g = lane >> 4;
-  const __amdgpu_buffer_rsrc_t rs = mzw_rsrc(L.s), rb = mzw_rsrc(L.b1), r32 = mzw_rsrc(L.w32);
   const int vs = 16 * lane, vb = 16 * g;  // byte offsets: the lane's fragment slot, its group's 4 biases
 #pragma unroll
   for (int ot = 0; ot < NO; ++ot)
@@ -138,16 +139,16 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[N
   // the compiler from sinking the refills to their uses.
   floatx4 w[FR];
 #pragma unroll
-  for (int f = 0; f < FR; ++f) w[f] = mzw_ld4(rs, vs, f * 1024);
+  for (int f = 0; f < FR; ++f) w[f] = mzw_ld4(rw, vs, L.soff + f * 1024);
   float a32[NT];
 #pragma unroll
   for (int n = 0; n < NT; ++n) a32[n] = 0.0f;
 #pragma unroll 2
   for (int ht = 0; ht < 16; ++ht) {
-    const int sn = (ht + 1) * FR * 1024;  // next block's byte offset (block 16 is the zero pad)
-    const floatx4 b = mzw_ld4(rb, vb, 64 * ht);
+    const int sn = L.soff + (ht + 1) * FR * 1024;  // next block's byte offset (block 16 is the zero pad)
+    const floatx4 b = mzw_ld4(rw, vb, L.b1off + 64 * ht);
     floatx4 w32 = {0.f, 0.f, 0.f, 0.f};
-    if (B32) w32 = mzw_ld4(r32, vb, 64 * ht);
+    if (B32) w32 = mzw_ld4(rw, vb, L.w32off + 64 * ht);
     floatx4 o[NT];
 #pragma unroll
     for (int n = 0; n < NT; ++n)
@@ -162,7 +163,7 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[N
 #pragma unroll
         for (int n = 0; n < NT; ++n)
           acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[kb][t], x[n][kb][t], acc[n], 0, 0, 0);
-      w[kb] = mzw_ld4(rs, vs, sn + kb * 1024);
+      w[kb] = mzw_ld4(rw, vs, sn + kb * 1024);
       __builtin_amdgcn_sched_barrier(0);
     }
     floatx4 hid[NT];
@@ -189,7 +190,7 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[N
       }
     }
 #pragma unroll
-    for (int ot = 0; ot < NO; ++ot) w[KB1 + ot] = mzw_ld4(rs, vs, sn + (KB1 + ot) * 1024);
+    for (int ot = 0; ot < NO; ++ot) w[KB1 + ot] = mzw_ld4(rw, vs, sn + (KB1 + ot) * 1024);
     __builtin_amdgcn_sched_barrier(0);
   }
   if (B32) {
@@ -199,10 +200,10 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, const floatx4 (&x)[N
 }
 
 template <int NT, int NO>
-__device__ __forceinline__ void mzw_bias2(const MzhWMlp& L, floatx4 (&out)[NO][NT], int g) {
+__device__ __forceinline__ void mzw_bias2(const MzhWMlp& L, __amdgpu_buffer_rsrc_t rw, floatx4 (&out)[NO][NT], int g) {
 #pragma unroll
   for (int ot = 0; ot < NO; ++ot) {
-    const floatx4 b = *reinterpret_cast<const floatx4*>(L.b2 + 16 * ot + 4 * g);
+    const floatx4 b = mzw_ld4(rw, 16 * g, L.b2off + 64 * ot);
 #pragma unroll
     for (int n = 0; n < NT; ++n)
 #pragma unroll
@@ -408,6 +409,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (scalar branches)
   const int g = lane >> 4, col = lane & 15;
+  const __amdgpu_buffer_rsrc_t rw = mzw_rsrc(net.wbase);
 
   if (!REPLAY)
     for (int i = tid; i < MZH_A * MZH_F; i += MZW_WAVES * 64) ohl[i] = net.oh[i];
@@ -467,12 +469,12 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
         }
     floatx4 hp[4][NT];
     switch (net.rep.kb1) {
-      case 1: mzw_chain<NT, 1, 4, false>(net.rep, x, noh, hp, lane); break;
-      case 2: mzw_chain<NT, 2, 4, false>(net.rep, x, noh, hp, lane); break;
-      case 3: mzw_chain<NT, 3, 4, false>(net.rep, x, noh, hp, lane); break;
-      default: mzw_chain<NT, 4, 4, false>(net.rep, x, noh, hp, lane); break;
+      case 1: mzw_chain<NT, 1, 4, false>(net.rep, rw, x, noh, hp, lane); break;
+      case 2: mzw_chain<NT, 2, 4, false>(net.rep, rw, x, noh, hp, lane); break;
+      case 3: mzw_chain<NT, 3, 4, false>(net.rep, rw, x, noh, hp, lane); break;
+      default: mzw_chain<NT, 4, 4, false>(net.rep, rw, x, noh, hp, lane); break;
     }
-    mzw_bias2<NT, 4>(net.rep, hp, g);
+    mzw_bias2<NT, 4>(net.rep, rw, hp, g);
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
       mzw_normalize<NT>(hp, n, hreg);
@@ -483,10 +485,10 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
       }
     }
     floatx4 pl[1][NT];
-    mzw_chain<NT, 4, 1, false>(net.pol, hreg, noh, pl, lane);
-    mzw_bias2<NT, 1>(net.pol, pl, g);
+    mzw_chain<NT, 4, 1, false>(net.pol, rw, hreg, noh, pl, lane);
+    mzw_bias2<NT, 1>(net.pol, rw, pl, g);
     floatx4 vl[NOV][NT];
-    mzw_chain<NT, 4, NOV, false>(net.val, hreg, noh, vl, lane);  // root value: computed, unused (mcts.py:50)
+    mzw_chain<NT, 4, NOV, false>(net.val, rw, hreg, noh, vl, lane);  // root value: computed, unused (mcts.py:50)
     (void)vl;
 #pragma unroll
     for (int n = 0; n < NT; ++n) rpi[n] = mzw_policy(pl[0][n], lane);
@@ -704,16 +706,16 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
     const float* ohp[NT];
 #pragma unroll
     for (int n = 0; n < NT; ++n) ohp[n] = ohl + an[n] * MZH_F + 4 * g;
-    mzw_chain<NT, 4, 4, true>(net.dyn, x, ohp, hp, lane);
-    mzw_bias2<NT, 4>(net.dyn, hp, g);  // h' (un-normalised, networks.py:129-138)
+    mzw_chain<NT, 4, 4, true>(net.dyn, rw, x, ohp, hp, lane);
+    mzw_bias2<NT, 4>(net.dyn, rw, hp, g);  // h' (un-normalised, networks.py:129-138)
     floatx4 hx[NT][4];
 #pragma unroll
     for (int n = 0; n < NT; ++n)
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) hx[n][kb] = hp[kb][n];
     float r32[NT], v32[NT];
-    mzw_chain<NT, 4, NOV, false, SUP33>(net.rwd, hx, noh, rl, lane, r32);  // reward from h' (networks.py:132-135)
-    mzw_bias2<NT, NOV>(net.rwd, rl, g);
+    mzw_chain<NT, 4, NOV, false, SUP33>(net.rwd, rw, hx, noh, rl, lane, r32);  // reward from h' (networks.py:132-135)
+    mzw_bias2<NT, NOV>(net.rwd, rw, rl, g);
 #pragma unroll
     for (int n = 0; n < NT; ++n) rew[n] = mzw_head<NT, NOV>(rl, n, lane, SUP33 ? r32[n] : 0.0f, net.rwd.b32);
 #pragma unroll
@@ -725,12 +727,12 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
         for (int kb = 0; kb < 4; ++kb) dst[4 * kb] = hreg[n][kb];
       }
     }
-    mzw_chain<NT, 4, 1, false>(net.pol, hreg, noh, pl, lane);
-    mzw_bias2<NT, 1>(net.pol, pl, g);
+    mzw_chain<NT, 4, 1, false>(net.pol, rw, hreg, noh, pl, lane);
+    mzw_bias2<NT, 1>(net.pol, rw, pl, g);
 #pragma unroll
     for (int n = 0; n < NT; ++n) cpi[n] = mzw_policy(pl[0][n], lane);
-    mzw_chain<NT, 4, NOV, false, SUP33>(net.val, hreg, noh, vl, lane, v32);
-    mzw_bias2<NT, NOV>(net.val, vl, g);
+    mzw_chain<NT, 4, NOV, false, SUP33>(net.val, rw, hreg, noh, vl, lane, v32);
+    mzw_bias2<NT, NOV>(net.val, rw, vl, g);
 #pragma unroll
     for (int n = 0; n < NT; ++n) val[n] = mzw_head<NT, NOV>(vl, n, lane, SUP33 ? v32[n] : 0.0f, net.val.b32);
   };
