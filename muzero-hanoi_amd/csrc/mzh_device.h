@@ -791,12 +791,12 @@ __device__ __forceinline__ MzhHeadOut mzh_heads_row(SM& sm, const MzhNet& net, i
       // bin 32 (lane 0, i = 4) from the vector chains above
       const float raw = (CHAIN32 && i == 4) ? (h ? l32r : l32v) : lv[h][k];
       e[h][i] = (h < nh && k < 33) ? raw : -__builtin_inff();
-      m[h] = e[h][i] > m[h] ? e[h][i] : m[h];
+      m[h] = __builtin_fmaxf(e[h][i], m[h]);  // NaN-free; the max only feeds exponent arguments
     }
   }
-  const float mp = mzh_max8(lg);
+  const float mp = mzh_max8_nonan(lg);
 #pragma unroll
-  for (int h = 0; h < 2; ++h) m[h] = mzh_max8(m[h]);
+  for (int h = 0; h < 2; ++h) m[h] = mzh_max8_nonan(m[h]);
   // every exponent argument is <= 0; xmin tracks the smallest one that feeds a probability
   const float xp = lg - mp;
   const float epx = mzh_expf_np(xp);  // every lane (no divergent branch); lanes 6, 7 discard it
@@ -809,7 +809,7 @@ __device__ __forceinline__ MzhHeadOut mzh_heads_row(SM& sm, const MzhNet& net, i
       const float xv = e[h][i] - m[h];
       const float ex = mzh_expf_np(xv);  // every lane (no divergent branch)
       e[h][i] = (q + 8 * i < 33) ? ex : 0.0f;
-      if (h < nh && q + 8 * i < 33) xmin = xv < xmin ? xv : xmin;
+      if (h < nh && q + 8 * i < 33) xmin = __builtin_fminf(xv, xmin);
     }
   float sh[2];
 #pragma unroll

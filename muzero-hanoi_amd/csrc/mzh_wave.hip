@@ -79,12 +79,15 @@ __device__ __forceinline__ void mzw_pair32(float v, float& a, float& b) {
   a = __uint_as_float(r[0]);
   b = __uint_as_float(r[1]);
 }
+// The maxima below feed only exponent arguments (x - max: identical for a +0 / -0 max), the
+// normaliser's max - min (likewise) and argmax equality masks, and no operand is NaN: v_max_f32
+// (one instruction) instead of compare + select (two, with a VCC hazard wait between them).
 __device__ __forceinline__ float mzw_max4g(float v) {  // max over the 4 lane groups (rows) of a column
   float a, b;
   mzw_pair16(v, a, b);
-  v = a > b ? a : b;
+  v = __builtin_fmaxf(a, b);
   mzw_pair32(v, a, b);
-  return a > b ? a : b;
+  return __builtin_fmaxf(a, b);
 }
 __device__ __forceinline__ float mzw_min4g(float v) {
   float a, b;
@@ -260,8 +263,8 @@ __device__ __forceinline__ float mzw_head(const floatx4 (&l)[NO][NT], int n, int
   L[8] = mzw_add32(mzw_add16(p32)) + b32;  // ((p0 + p1) + (p2 + p3)) + bias: bin 32 on every group
   float m = L[0];
 #pragma unroll
-  for (int s = 1; s < 8; ++s) m = L[s] > m ? L[s] : m;
-  if (v8) m = L[8] > m ? L[8] : m;
+  for (int s = 1; s < 8; ++s) m = __builtin_fmaxf(L[s], m);
+  if (v8) m = __builtin_fmaxf(L[8], m);
   m = mzw_max4g(m);
   float e[9];
 #pragma unroll
@@ -281,10 +284,20 @@ __device__ __forceinline__ float mzw_head(const floatx4 (&l)[NO][NT], int n, int
   t = mzw_add16(t);  // (s0+s1)+(s2+s3) | (s4+s5)+(s6+s7)
   t = mzw_add32(t);
   const float y = 1.0f / t;
-  bool slow = false;
+  // Markstein quotients, exact while every used exponent argument is >= -65 (t lies in [1, 33], so
+  // each numerator is >= e^-65 and each quotient > 2^-100: mzh_fdiv's condition, decided once per
+  // lane from the smallest logit); otherwise the wave takes IEEE divisions
+  float lmin = L[0];
+#pragma unroll
+  for (int s = 1; s < 8; ++s) lmin = __builtin_fminf(L[s], lmin);
+  if (v8) lmin = __builtin_fminf(L[8], lmin);
+  const bool slow = lmin - m < -65.0f;
   float pk[9];
 #pragma unroll
-  for (int s = 0; s < 9; ++s) pk[s] = mzh_fdiv(e[s], t, y, slow);
+  for (int s = 0; s < 9; ++s) {
+    const float q = e[s] * y;
+    pk[s] = __builtin_fmaf(__builtin_fmaf(-q, t, e[s]), y, q);
+  }
   if (__builtin_expect(__ballot(slow) != 0, 0)) {
 #pragma unroll
     for (int s = 0; s < 9; ++s) pk[s] = e[s] / t;
@@ -315,12 +328,12 @@ __device__ __forceinline__ floatx4 mzw_policy(const floatx4 l, int lane) {
   const bool ok01 = g < 2, ok23 = g == 0;
   float m = -__builtin_inff();
   if (ok01) {
-    m = l[0] > m ? l[0] : m;
-    m = l[1] > m ? l[1] : m;
+    m = __builtin_fmaxf(l[0], m);
+    m = __builtin_fmaxf(l[1], m);
   }
   if (ok23) {
-    m = l[2] > m ? l[2] : m;
-    m = l[3] > m ? l[3] : m;
+    m = __builtin_fmaxf(l[2], m);
+    m = __builtin_fmaxf(l[3], m);
   }
   m = mzw_max4g(m);
   // arguments <= 0 on the lanes whose result is used; evaluated on every lane (no divergent branch)
@@ -331,12 +344,20 @@ __device__ __forceinline__ floatx4 mzw_policy(const floatx4 l, int lane) {
   float t = (e0 + e1) + (e2 + e3);
   t = mzw_add16(t);  // group 0: ((s0+s1)+(s2+s3)) + ((s4+s5)+(0+0))
   const float y = 1.0f / t;
-  bool slow = false;
+  // exactness of the Markstein quotients decided once per lane, as in mzw_head (t lies in [1, 6])
+  float lmin = __builtin_inff();
+  if (ok01) lmin = __builtin_fminf(__builtin_fminf(l[0], l[1]), lmin);
+  if (ok23) lmin = __builtin_fminf(__builtin_fminf(l[2], l[3]), lmin);
+  const bool slow = lmin - m < -65.0f;
+  auto mdiv = [&](float a) {
+    const float q = a * y;
+    return __builtin_fmaf(__builtin_fmaf(-q, t, a), y, q);
+  };
   floatx4 p;
-  p[0] = mzh_fdiv(e0, t, y, slow);
-  p[1] = mzh_fdiv(e1, t, y, slow);
-  p[2] = mzh_fdiv(e2, t, y, slow);
-  p[3] = mzh_fdiv(e3, t, y, slow);
+  p[0] = mdiv(e0);
+  p[1] = mdiv(e1);
+  p[2] = mdiv(e2);
+  p[3] = mdiv(e3);
   if (__builtin_expect(__ballot(slow) != 0, 0)) {
     p[0] = e0 / t;
     p[1] = e1 / t;
@@ -374,11 +395,11 @@ __device__ __forceinline__ float mzw_ucb(int Nc, double Wc, float Rc, double P64
 // both lanes return the same pick and tie bookkeeping
 __device__ __forceinline__ int mzw_pick_pair(const float (&u)[3], int half, int tie, int& firstTie, int& extra) {
   float m = u[0];
-  m = u[1] > m ? u[1] : m;
-  m = u[2] > m ? u[2] : m;
+  m = __builtin_fmaxf(u[1], m);
+  m = __builtin_fmaxf(u[2], m);
   float a, b;
   mzw_pair32(m, a, b);
-  const float M = a > b ? a : b;
+  const float M = __builtin_fmaxf(a, b);
   int mask = 0;
 #pragma unroll
   for (int j = 0; j < 3; ++j) mask |= (u[j] == M ? 1 : 0) << j;
