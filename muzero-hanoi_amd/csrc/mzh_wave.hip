@@ -548,6 +548,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
   float val[NT], rew[NT];
   floatx4 cpi[NT];
 
+  MZH_STAMP_DECL  // diagnostic build: phase stamps (the M phase's are 5-9, see tools/wave_probe.py)
   // select one leaf per root, then hand its parent latent index / move to the column lanes
   // ex: MzhBool<true> = the exact (IEEE-division) normaliser, for a wave where some root's max - min
   // is a non-zero subnormal (caller-given bounds only); chosen once per selection
@@ -727,8 +728,10 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
     const float* ohp[NT];
 #pragma unroll
     for (int n = 0; n < NT; ++n) ohp[n] = ohl + an[n] * MZH_F + 4 * g;
+    MZH_STAMP(10);  // latent gather
     mzw_chain<NT, 4, 4, true>(net.dyn, rw, x, ohp, hp, lane);
     mzw_bias2<NT, 4>(net.dyn, rw, hp, g);  // h' (un-normalised, networks.py:129-138)
+    MZH_STAMP(5);
     floatx4 hx[NT][4];
 #pragma unroll
     for (int n = 0; n < NT; ++n)
@@ -738,7 +741,10 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
     mzw_chain<NT, 4, NOV, false, SUP33>(net.rwd, rw, hx, noh, rl, lane, r32);  // reward from h' (networks.py:132-135)
     mzw_bias2<NT, NOV>(net.rwd, rw, rl, g);
 #pragma unroll
+    MZH_STAMP(6);
+#pragma unroll
     for (int n = 0; n < NT; ++n) rew[n] = mzw_head<NT, NOV>(rl, n, lane, SUP33 ? r32[n] : 0.0f, net.rwd.b32);
+    MZH_STAMP(11);
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
       mzw_normalize<NT>(hp, n, hreg);
@@ -748,12 +754,15 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
         for (int kb = 0; kb < 4; ++kb) dst[4 * kb] = hreg[n][kb];
       }
     }
+    MZH_STAMP(7);
     mzw_chain<NT, 4, 1, false>(net.pol, rw, hreg, noh, pl, lane);
     mzw_bias2<NT, 1>(net.pol, rw, pl, g);
 #pragma unroll
     for (int n = 0; n < NT; ++n) cpi[n] = mzw_policy(pl[0][n], lane);
+    MZH_STAMP(8);
     mzw_chain<NT, 4, NOV, false, SUP33>(net.val, rw, hreg, noh, vl, lane, v32);
     mzw_bias2<NT, NOV>(net.val, rw, vl, g);
+    MZH_STAMP(9);
 #pragma unroll
     for (int n = 0; n < NT; ++n) val[n] = mzw_head<NT, NOV>(vl, n, lane, SUP33 ? v32[n] : 0.0f, net.val.b32);
   };
@@ -903,7 +912,6 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
     }
   };
 
-  MZH_STAMP_DECL
   for (int s = 0; s < S; ++s) {
     MZH_STAMP(4);
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(rvalid && mmax > mmin && !(den >= 2.2250738585072014e-308)) != 0, 0))

@@ -14,7 +14,9 @@ import torch  # noqa: E402
 from muzero_hanoi_amd import _lib, engine, rng  # noqa: E402
 from muzero_hanoi_amd.networks import MuZeroNet  # noqa: E402
 
-PH = {0: "select", 1: "mlp", 2: "head+backup", 3: "barrier", 4: "loop-top"}
+PH = {0: "select", 1: "mlp (value head)", 2: "head+backup", 3: "barrier", 4: "loop-top",
+      10: "mlp: latent gather", 5: "mlp: dynamics chain", 6: "mlp: reward chain", 11: "mlp: reward head",
+      7: "mlp: normalise + latent store", 8: "mlp: policy chain + softmax", 9: "mlp: value chain"}
 
 
 def main():
@@ -36,7 +38,7 @@ def main():
     eng.search(S, obs=obs, tie_idx=tie, noise=noise, action_u=u, kernel=os.environ.get("MZH_PROBE_KERNEL", "wave"))
     torch.cuda.synchronize()
     L.mzh_diag_wave_stamps(buf.ctypes.data)
-    per = buf[:8, :5] / S  # 8 waves (ping-pong workgroup); the 4-wave build leaves rows 4-7 zero
+    per = buf[:8, :12] / S  # 8 waves (ping-pong workgroup); the 4-wave build leaves rows 4-7 zero
     out = {f"{k}:{v}": [round(x) for x in per[:, k]] for k, v in PH.items()}
     out["total"] = [round(x) for x in per.sum(1)]
     print(json.dumps(out))
