@@ -583,11 +583,12 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
         int nx;
         double Wp;
         float Rp;
-        if constexpr (NT == 1) {
-          // 16-root waves: this lane's half of the block only -- its three children's N|X, R, P and
-          // W (5 loads, 60 B, instead of the whole 128-B line on both lanes); the picked child's
-          // fields come from the lane that holds them over v_permlane32_swap (16,384 roots -1.4%;
-          // at 32 roots per wave the extra registers spill: +1.6%, so NT = 2 loads the line)
+        {
+          // this lane's half of the block only -- its three children's N|X, R, P and W (5 loads,
+          // 60 B, instead of the whole 128-B line on both lanes and a select of each field by half);
+          // the picked child's fields come from the lane that holds them over v_permlane32_swap
+          // (16,384 roots -1.4%; at 32 roots per wave, once the buffer-load weight stream freed the
+          // registers it spilled in round 3: 65,536 roots -0.9%, 262,144 -1.3%)
           const unsigned char* blk = reinterpret_cast<const unsigned char*>(&tb[e]);
           const uint3 hnx = *reinterpret_cast<const uint3*>(blk + 12 * half);
           const uint3 hR = *reinterpret_cast<const uint3*>(blk + 24 + 12 * half);
@@ -634,54 +635,6 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
           Rp = __uint_as_float(take(__float_as_uint(cr)));
           const long long wb = __double_as_longlong(cw);
           Wp = __hiloint2double((int)take((unsigned)(wb >> 32)), (int)take((unsigned)(wb & 0xFFFFFFFFll)));
-        } else {
-          const int4* bp = reinterpret_cast<const int4*>(&tb[e]);
-          int dw[32];
-  #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const int4 q = bp[k];
-            dw[4 * k] = q.x;
-            dw[4 * k + 1] = q.y;
-            dw[4 * k + 2] = q.z;
-            dw[4 * k + 3] = q.w;
-          }
-          if (kPF) {
-            // retire the previous level's child prefetches (older than this block's loads), then
-            // touch this lane's three children's blocks: the next level's block is one of them
-            asm volatile("" ::"v"(pf0), "v"(pf1), "v"(pf2));
-            const int x0 = (half ? dw[3] : dw[0]) >> 16, x1 = (half ? dw[4] : dw[1]) >> 16, x2 = (half ? dw[5] : dw[2]) >> 16;
-            pf0 = *reinterpret_cast<const int*>(&tb[x0 >= 0 ? x0 : e]);
-            pf1 = *reinterpret_cast<const int*>(&tb[x1 >= 0 ? x1 : e]);
-            pf2 = *reinterpret_cast<const int*>(&tb[x2 >= 0 ? x2 : e]);
-          }
-          double Wc[6];
-          float Rc[6];
-  #pragma unroll
-          for (int c = 0; c < MZH_A; ++c) {
-            Rc[c] = __int_as_float(dw[6 + c]);
-            Wc[c] = __hiloint2double(dw[19 + 2 * c], dw[18 + 2 * c]);
-          }
-          const double tn = table[Np];
-  #pragma unroll
-          for (int j = 0; j < 3; ++j) {
-            // this lane's three children (dw is the whole block on both lanes)
-            const int nxj = half ? dw[3 + j] : dw[j];
-            const float Rj = half ? Rc[3 + j] : Rc[j];
-            const double Wj = half ? Wc[3 + j] : Wc[j];
-            const float Pj = __int_as_float(half ? dw[15 + j] : dw[12 + j]);
-            u[j] = mzw_ucb(nxj & 0xFFFF, Wj, Rj, (double)Pj, p.np1, tn, disc, has, mmin, den, dinv, inv, exact);
-          }
-          pick = mzw_pick_pair(u, half, tie, firstTie, extra);
-          nx = dw[0];
-          Wp = Wc[0];
-          Rp = Rc[0];
-  #pragma unroll
-          for (int c = 1; c < MZH_A; ++c)
-            if (pick == c) {
-              nx = dw[c];
-              Wp = Wc[c];
-              Rp = Rc[c];
-            }
         }
         Np = nx & 0xFFFF;
         X = nx >> 16;
