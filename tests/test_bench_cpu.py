@@ -102,3 +102,38 @@ def test_tree_latency_floor():
     pw = bench.search_plan(S, 262144)  # wave kernel: 32-root waves, 8,192 waves = 4 rounds of 2,048 slots
     f = bench.tree_latency_floor(np.full(262144, 2 * S), S, pw, load_ns=100.0)
     assert f["roots_per_group"] == 32 and f["rounds"] == 4 and abs(f["floor_ms"] - 4 * S * 1 * 100e-6) < 1e-12
+
+
+def test_traffic_summary_keeps_the_bench_instantiation(tmp_path):
+    """tools/traffic.py: a profiled bench command that also launched another instantiation of the
+    same kernel (the minmax_in leg's MMIN = true) summarises the bench's own instantiation as
+    'fused' and lists the other under 'other', kept out of the PMC figures"""
+    import csv
+
+    import traffic
+
+    bench_k = "mzh_search_kernel<32, false, true, true, false>"
+    other_k = "mzh_search_kernel<32, false, true, true, true>"
+    tree_k = "mzh_search_kernel<32, true, false, true, false>"
+    full = lambda k: f"void {k}(MzhNet, MzhSearchParams)"  # noqa: E731
+    d = tmp_path / "prof_t_trace" / "run"
+    d.mkdir(parents=True)
+    with open(d / "1_kernel_stats.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Name", "Calls", "AverageNs"])
+        w.writerow([full(bench_k), 12, 1300000.0])
+        w.writerow([full(other_k), 6, 1250000.0])  # listed after the bench's: must not overwrite it
+        w.writerow([full(tree_k), 12, 250000.0])
+    d = tmp_path / "prof_t_fetch" / "run"
+    d.mkdir(parents=True)
+    with open(d / "1_counter_collection.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Counter_Name", "Dispatch_Id", "Counter_Value"])
+        for disp, k, v in ((1, bench_k, 100.0), (2, bench_k, 100.0), (3, other_k, 999.0), (4, tree_k, 10.0)):
+            for xcd in range(2):  # per-XCD rows of one dispatch are summed
+                w.writerow([full(k), "FETCH_SIZE", disp, v / 2])
+    out = traffic.summarise(str(tmp_path), "t", {"fused": bench_k, "tree": tree_k})
+    assert out["fused"]["kernel"] == full(bench_k) and out["fused"]["avg_ns"] == 1300000.0
+    assert out["fused"]["FETCH_SIZE"] == 100.0 and out["fused"]["hbm_read_bytes_corrected"] == 100.0 * 1024 * 2
+    assert out["tree"]["kernel"] == full(tree_k) and out["tree"]["FETCH_SIZE"] == 10.0
+    assert list(out["other"]) == [full(other_k)]
