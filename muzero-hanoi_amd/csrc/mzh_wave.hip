@@ -89,12 +89,14 @@ __device__ __forceinline__ float mzw_max4g(float v) {  // max over the 4 lane gr
   mzw_pair32(v, a, b);
   return __builtin_fmaxf(a, b);
 }
+// min over the 4 lane groups for the latent normalisation: no operand is NaN or -0 (a latent unit is
+// an FMA chain from +0 plus a bias, which never rounds to -0), so v_min_f32 is the select's result
 __device__ __forceinline__ float mzw_min4g(float v) {
   float a, b;
   mzw_pair16(v, a, b);
-  v = a < b ? a : b;
+  v = __builtin_fminf(a, b);
   mzw_pair32(v, a, b);
-  return a < b ? a : b;
+  return __builtin_fminf(a, b);
 }
 __device__ __forceinline__ float mzw_add16(float v) {  // row0 + row1 (row2 + row3)
   float a, b;
@@ -223,8 +225,8 @@ __device__ __forceinline__ void mzw_normalize(const floatx4 (&hp)[4][NT], int n,
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float v = hp[ot][n][i];
-      mn = v < mn ? v : mn;
-      mx = v > mx ? v : mx;
+      mn = __builtin_fminf(v, mn);  // NaN- and -0-free (see mzw_min4g)
+      mx = __builtin_fmaxf(v, mx);
     }
   mn = mzw_min4g(mn);
   mx = mzw_max4g(mx);
