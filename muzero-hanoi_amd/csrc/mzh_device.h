@@ -190,6 +190,25 @@ __device__ __forceinline__ float mzh_max8_nonan(float v) {
   asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %1, %1 row_half_mirror row_mask:0xf bank_mask:0xf" : "=v"(c) : "v"(b));
   return c;
 }
+// NaN- and -0-free operands (the latent normalisation's raw units: an FMA chain from +0 plus a bias
+// never rounds to -0): v_min / v_max, no compare + select, no canonicalising of LDS-loaded operands
+__device__ __forceinline__ float mzh_vmin(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float mzh_vmax(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float mzh_min8_nonan(float v) {
+  float a, b, c;
+  asm volatile("s_nop 1\n\tv_min_f32_dpp %0, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(a) : "v"(v));
+  asm volatile("s_nop 1\n\tv_min_f32_dpp %0, %1, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf" : "=v"(b) : "v"(a));
+  asm volatile("s_nop 1\n\tv_min_f32_dpp %0, %1, %1 row_half_mirror row_mask:0xf bank_mask:0xf" : "=v"(c) : "v"(b));
+  return c;
+}
 __device__ __forceinline__ float mzh_min8(float v) {
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
@@ -674,16 +693,16 @@ struct MzhNormPass {
       float lo = v[k][0], hi = v[k][0];
 #pragma unroll
       for (int i = 1; i < NE; ++i) {
-        lo = v[k][i] < lo ? v[k][i] : lo;
-        hi = v[k][i] > hi ? v[k][i] : hi;
+        lo = mzh_vmin(v[k][i], lo);
+        hi = mzh_vmax(v[k][i], hi);
       }
-      lo = mzh_min8(lo);
-      hi = mzh_max8(hi);
+      lo = mzh_min8_nonan(lo);
+      hi = mzh_max8_nonan(hi);
       if (R == 16) {  // the two 8-lane halves of the row (row_ror:8)
         const float tn = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(lo), 0x128, 0xF, 0xF, true));
         const float tx = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(hi), 0x128, 0xF, 0xF, true));
-        lo = tn < lo ? tn : lo;
-        hi = tx > hi ? tx : hi;
+        lo = mzh_vmin(tn, lo);
+        hi = mzh_vmax(tx, hi);
       }
       mn[k] = lo;
       d[k] = (hi - lo) + 9.999999939225290290778502821922302246094e-09f;
