@@ -127,11 +127,15 @@ __device__ __forceinline__ floatx4 mzw_ld4(__amdgpu_buffer_rsrc_t r, int voff, i
 }
 
 // rw: the blob's buffer resource (MzhWNet::wbase, made once per kernel: one SGPR quad for every chain)
-template <int NT, int KB1, int NO, bool OH, bool B32 = false>
+// Chained form (WS > 0): the rolling buffer is the caller's wst[WS], which arrives holding this chain's
+// block 0 (loaded by the previous chain), and the last block's refills load the NEXT chain's block 0
+// (fragments 0..WS-1 at byte offset next_soff) instead of the zero pad, so no chain starts on an L2 round trip.
+template <int NT, int KB1, int NO, bool OH, bool B32 = false, int WS = 0>
 __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, __amdgpu_buffer_rsrc_t rw, const floatx4 (&x)[NT][4],
                                           const float* const (&oh)[NT], floatx4 (&out)[NO][NT], int lane,
-                                          float* p32 = nullptr) {
+                                          float* p32 = nullptr, floatx4* wst = nullptr, int next_soff = 0) {
   constexpr int FR = KB1 + NO;
+  static_assert(WS == 0 || WS >= FR, "chained buffer too small");
   const int g = lane >> 4;
   const int vs = 16 * lane, vb = 16 * g;  // byte offsets: the lane's fragment slot, its group's 4 biases
 #pragma unroll
@@ -142,15 +146,19 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, __amdgpu_buffer_rsrc
   // with fragment f of the next block as soon as its MFMAs are issued, so every load has the rest
   // of this block's MFMAs (and the next block's up to f) to land.  The scheduling barriers keep
   // the compiler from sinking the refills to their uses.
-  floatx4 w[FR];
+  floatx4 wloc[WS > 0 ? 1 : FR];
+  floatx4* w = WS > 0 ? wst : wloc;
+  if constexpr (WS == 0) {
 #pragma unroll
-  for (int f = 0; f < FR; ++f) w[f] = mzw_ld4(rw, vs, L.soff + f * 1024);
+    for (int f = 0; f < FR; ++f) w[f] = mzw_ld4(rw, vs, L.soff + f * 1024);
+  }
   float a32[NT];
 #pragma unroll
   for (int n = 0; n < NT; ++n) a32[n] = 0.0f;
 #pragma unroll 2
   for (int ht = 0; ht < 16; ++ht) {
-    const int sn = L.soff + (ht + 1) * FR * 1024;  // next block's byte offset (block 16 is the zero pad)
+    // next block's byte offset (block 16 is the zero pad; chained: the next chain's block 0)
+    const int sn = (WS > 0 && ht == 15) ? next_soff : L.soff + (ht + 1) * FR * 1024;
     const floatx4 b = mzw_ld4(rw, vb, L.b1off + 64 * ht);
     floatx4 w32 = {0.f, 0.f, 0.f, 0.f};
     if (B32) w32 = mzw_ld4(rw, vb, L.w32off + 64 * ht);
@@ -197,6 +205,10 @@ __device__ __forceinline__ void mzw_chain(const MzhWMlp& L, __amdgpu_buffer_rsrc
 #pragma unroll
     for (int ot = 0; ot < NO; ++ot) w[KB1 + ot] = mzw_ld4(rw, vs, sn + (KB1 + ot) * 1024);
     __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (WS > FR) {  // the next chain's fragments past this chain's slots
+#pragma unroll
+    for (int f = FR; f < WS; ++f) w[f] = mzw_ld4(rw, vs, next_soff + f * 1024);
   }
   if (B32) {
 #pragma unroll
@@ -550,6 +562,12 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
   float val[NT], rew[NT];
   floatx4 cpi[NT];
 
+  // the four recurrent chains' rolling weight buffer, handed from chain to chain (mzw_chain WS)
+  floatx4 wst[8];
+  if (!REPLAY) {
+#pragma unroll
+    for (int f = 0; f < 8; ++f) wst[f] = mzw_ld4(rw, 16 * lane, net.dyn.soff + f * 1024);
+  }
   MZH_STAMP_DECL  // diagnostic build: phase stamps (the M phase's are 5-9, see tools/wave_probe.py)
   // select one leaf per root, then hand its parent latent index / move to the column lanes
   // ex: MzhBool<true> = the exact (IEEE-division) normaliser, for a wave where some root's max - min
@@ -684,7 +702,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
 #pragma unroll
     for (int n = 0; n < NT; ++n) ohp[n] = ohl + an[n] * MZH_F + 4 * g;
     MZH_STAMP(10);  // latent gather
-    mzw_chain<NT, 4, 4, true>(net.dyn, rw, x, ohp, hp, lane);
+    mzw_chain<NT, 4, 4, true, false, 8>(net.dyn, rw, x, ohp, hp, lane, nullptr, wst, net.rwd.soff);
     mzw_bias2<NT, 4>(net.dyn, rw, hp, g);  // h' (un-normalised, networks.py:129-138)
     MZH_STAMP(5);
     floatx4 hx[NT][4];
@@ -693,7 +711,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) hx[n][kb] = hp[kb][n];
     float r32[NT], v32[NT];
-    mzw_chain<NT, 4, NOV, false, SUP33>(net.rwd, rw, hx, noh, rl, lane, r32);  // reward from h' (networks.py:132-135)
+    mzw_chain<NT, 4, NOV, false, SUP33, 8>(net.rwd, rw, hx, noh, rl, lane, r32, wst, net.pol.soff);  // reward from h' (networks.py:132-135)
     mzw_bias2<NT, NOV>(net.rwd, rw, rl, g);
 #pragma unroll
     MZH_STAMP(6);
@@ -710,12 +728,12 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
       }
     }
     MZH_STAMP(7);
-    mzw_chain<NT, 4, 1, false>(net.pol, rw, hreg, noh, pl, lane);
+    mzw_chain<NT, 4, 1, false, false, 8>(net.pol, rw, hreg, noh, pl, lane, nullptr, wst, net.val.soff);
     mzw_bias2<NT, 1>(net.pol, rw, pl, g);
 #pragma unroll
     for (int n = 0; n < NT; ++n) cpi[n] = mzw_policy(pl[0][n], lane);
     MZH_STAMP(8);
-    mzw_chain<NT, 4, NOV, false, SUP33>(net.val, rw, hreg, noh, vl, lane, v32);
+    mzw_chain<NT, 4, NOV, false, SUP33, 8>(net.val, rw, hreg, noh, vl, lane, v32, wst, net.dyn.soff);  // + next dyn block 0
     mzw_bias2<NT, NOV>(net.val, rw, vl, g);
     MZH_STAMP(9);
 #pragma unroll
