@@ -1,3 +1,5 @@
+# HISTORICAL (record of profiles/r04_experiments.json): the 8-wave / phase-locked / priority variants it
+# compares were removed from the sources after the measurement (commit 83d898f); it no longer runs as written.
 # A/B: wave kernel 4-wave (drifting) vs 8-wave phase-locked workgroups; cooperative 32-root tile on 4 vs 8 waves
 set -e
 mkdir -p gpurun_out

@@ -1,3 +1,5 @@
+# HISTORICAL (record of profiles/r04_experiments.json): the 8-wave / phase-locked / priority variants it
+# compares were removed from the sources after the measurement (commit 83d898f); it no longer runs as written.
 # wave-kernel priority A/B (libmzh.so = MLP phase at priority 1; prio1 = tree phases at priority 1;
 # prio2 = no s_setprio), the cooperative tile's tree phase on 4 vs 8 waves, instruction mix at 65,536 roots
 set -e

@@ -1,3 +1,5 @@
+# HISTORICAL (record of profiles/r04_experiments.json): the 8-wave / phase-locked / priority variants it
+# compares were removed from the sources after the measurement (commit 83d898f); it no longer runs as written.
 # instruction mix of the wave kernel at configs[2] on one GPU (65,536 roots, NT=2) and its 16,384-root shard (NT=1)
 set -e
 bash tools/pmc_mix.sh "" c2 "mzh_wave_kernel<2, false" > /dev/null
