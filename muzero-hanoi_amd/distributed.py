@@ -77,6 +77,19 @@ def unpack_results(packed):
     return dict(visits=packed[:, :6], action=packed[:, 6], root_q=packed[:, 8:10].view(torch.float64).reshape(b))
 
 
+def gather_results_async(out, B, world):
+    """gather_results without waiting, for even shards (B % world == 0; None otherwise): returns
+    (work, rows, packed).  The packing runs on the current stream and the collective on the backend's
+    own stream after it, so the next search on the launch stream overlaps the all_gather; the caller
+    keeps the tuple alive and calls work.wait() before reading unpack_results(rows)."""
+    if B % world:
+        return None
+    packed = pack_results(out["visits"], out["action"], out["root_q"])
+    rows = torch.empty((B, PACK_WORDS), dtype=torch.int32, device=packed.device)
+    work = dist.all_gather_into_tensor(rows, packed, async_op=True)
+    return work, rows, packed
+
+
 def gather_results(out, B, world):
     """the global batch's visits [B, 6] int32, action [B] int32 and root_q [B] fp64 in root order,
     from every rank's search outputs (one all_gather of the packed rows)"""

@@ -44,8 +44,17 @@ def _worker(rank, world, port, B, out_path):
     noise, tie, u = rng.synthetic_draws(B, deterministic=False, alpha=0.25, seed=3)  # GLOBAL order
     sl = lambda x: mdist.shard(x, world, rank)
     o = orc.search(n, S, sl(obs), flat=flat, support=sup, noise=sl(noise), tie_idx=sl(tie), action_u=sl(u))
-    res = mdist.gather_results(dict(visits=torch.from_numpy(o["visits"]), action=torch.from_numpy(o["action"]),
-                                    root_q=torch.from_numpy(o["rootQ"])), B, world)
+    mine = dict(visits=torch.from_numpy(o["visits"]), action=torch.from_numpy(o["action"]),
+                root_q=torch.from_numpy(o["rootQ"]))
+    res = mdist.gather_results(mine, B, world)
+    # the overlapped form bench.py times (even shards only): the same rows once its work completes
+    pend = mdist.gather_results_async(mine, B, world)
+    if B % world:
+        assert pend is None
+    else:
+        pend[0].wait()
+        for k, v in mdist.unpack_results(pend[1]).items():
+            assert torch.equal(v, res[k]), k
     if rank == 0:
         np.savez(out_path, **{k: v.numpy() for k, v in res.items()})
     dist.destroy_process_group()
