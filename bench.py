@@ -3,6 +3,9 @@
     python bench.py [--gpus N --steps K --warmup W]                       # N=1
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W             # N>1, one rank per GPU
+    python bench.py --gpus N ...                                           # N>1 without a launcher:
+        bench.py starts torch.distributed.run itself as a child process (before anything touches
+        the GPU) and exits with its status, so the line always comes from N ranks
 
 Workload (default): BASELINE.json's metric batch, 65,536 random non-goal 4-disk root states x 50
 simulations, sharded contiguously over the N GPUs (strong scaling: 65,536 roots on 1 GPU, 8,192 per
@@ -105,7 +108,27 @@ def parse():
                    help="0: one process per physical core, capped at the GPU box's 16-CPU share per job")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    p.add_argument("--dry-run", action="store_true",
+                   help="rank plumbing only: start the ranks, form the process group, print the line's n_gpus / "
+                        "dist / shard fields without touching a GPU (tests/test_bench_cpu.py, gloo)")
     return p.parse_args()
+
+
+def relaunch_with_ranks(n):
+    """`--gpus N` (N > 1) started without a launcher: run the same command under
+    torch.distributed.run with N local ranks as a CHILD process (this process has not initialised
+    the GPU: no exec after a HIP call) and return its exit status"""
+    import socket
+    import subprocess
+
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"bench.py: --gpus {n} without a launcher; starting {n} ranks: {' '.join(cmd)}", file=sys.stderr,
+          flush=True)
+    return subprocess.run(cmd).returncode
 
 
 def random_roots(n_disks, B, seed):
@@ -313,21 +336,40 @@ def tree_latency_floor(sel_steps, S, plan, load_ns=None):
     mean over groups of max_r d_r x the measured dependent-load latency.  max of the per-root MEANS is
     below the mean of the per-simulation maxima, so this is a lower bound on the tree kernel's time."""
     load_ns = TREE_LOAD_NS if load_ns is None else load_ns
-    if load_ns is None:
-        return None
     d = np.asarray(sel_steps, np.float64) / S - 1.0
     g = plan["roots_per_wave"] if plan["wave"] else plan["roots_per_workgroup"]
     n = -(-len(d) // g)
     dd = np.zeros(n * g)
     dd[: len(d)] = d
     gmax = dd.reshape(n, g).max(1)
-    slots = 2048 if plan["wave"] else 256
+    slots = lockstep_slots(plan)
     rounds = -(-n // slots)
     floor_ms = rounds * S * float(gmax.mean()) * load_ns * 1e-6
     return {"floor_ms": floor_ms, "floor_ms_mall": floor_ms * TREE_LOAD_NS_MALL / load_ns,
             "groups": n, "roots_per_group": g, "rounds": rounds,
             "mean_group_max_loads_per_sim": float(gmax.mean()), "mean_loads_per_sim": float(d.mean()),
             "load_ns": load_ns, "load_footprint": TREE_LOAD_FOOTPRINT}
+
+
+CUS = 256                  # MI355X: 8 XCDs x 32 CUs
+LDS_PER_CU = 160 * 1024    # bytes
+
+
+def workgroups_per_cu(plan):
+    """co-resident workgroups per CU for a plan: its LDS footprint and its register budget -- the
+    wave kernel is built __launch_bounds__(256, 2) (<= 256 VGPRs: two waves per SIMD), the cooperative
+    kernel __launch_bounds__(256, 1) (one wave per SIMD); both use 4-wave workgroups"""
+    waves_per_simd_max = 2 if plan["wave"] else 1
+    by_lds = LDS_PER_CU // max(1, int(plan["smem_bytes"]))
+    by_regs = waves_per_simd_max * 4 // max(1, int(plan["threads_per_workgroup"]) // 64)
+    return max(1, min(by_lds, by_regs))
+
+
+def lockstep_slots(plan):
+    """lockstep groups the GPU runs at once: the wave kernel's waves (each a group of 16 NT roots),
+    the cooperative kernel's workgroups (each a group of R roots)"""
+    wg = CUS * workgroups_per_cu(plan)
+    return wg * (int(plan["threads_per_workgroup"]) // 64) if plan["wave"] else wg
 
 
 def waves_per_simd(plan, B):
@@ -341,11 +383,15 @@ def waves_per_simd(plan, B):
 
 def main():
     a = parse()
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(relaunch_with_ranks(a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world > 1:
-        raise SystemExit(f"--gpus {a.gpus} != WORLD_SIZE {world}")
+    if a.gpus != world:
+        raise SystemExit(f"--gpus {a.gpus} != WORLD_SIZE {world}: the line would not describe the ranks that ran")
     N, GB, S, desc = CONFIGS[a.config]
     N = a.disks or N
     S = a.sims or S
@@ -356,6 +402,10 @@ def main():
     srank, sworld = (rank, world) if a.shard is None else map(int, a.shard.split("/"))
     if a.shard is not None and (world > 1 or weak or not 0 <= srank < sworld):
         raise SystemExit("--shard R/W needs one process, no --roots-per-gpu, and 0 <= R < W")
+    if GB < max(world, sworld):
+        raise SystemExit(f"{GB} roots cannot give each of {max(world, sworld)} ranks a non-empty shard")
+    if a.dry_run:
+        return dry_run(a, world, rank, GB, S, N)
 
     # CPU baseline first (rank 0, N=1): spawned host processes, before this process touches the GPU
     cpu = None
@@ -395,7 +445,12 @@ def main():
     # inputs for the GLOBAL batch in global root order, then this rank's contiguous shard
     sl = lambda x: mdist.shard(x, sworld, srank)
     obs = torch.from_numpy(sl(random_roots(N, GB, a.seed))).to(dev)
-    noise, tie, u = rng.synthetic_draws(GB, deterministic=False, alpha=0.25, seed=a.seed)
+    # the reference's draws (Dirichlet noise, first-tie choice, action uniform) for the GLOBAL batch in
+    # reference order: what GB sequential run_mcts calls after np.random.seed(seed) consume
+    # (rng.predraw, libmzh's host restatement of NumPy's legacy stream), timed as host set-up
+    t_pd = time.perf_counter()
+    noise, tie, u = rng.predraw(GB, deterministic=False, alpha=0.25, rng=np.random.RandomState(a.seed))
+    predraw_ms = (time.perf_counter() - t_pd) * 1e3
     noise, tie, u = (torch.from_numpy(sl(x)).to(dev) for x in (noise, tie, u))
     out = eng.alloc_search_outputs(B, S)
     gather = dist is not None and not a.no_gather
@@ -609,6 +664,11 @@ def main():
                                                   "informational -- frac above is against the spec peak"},
                      "plan": plan, "with_minmax_in": mm, "tree": tree},
         "cpu_baseline": cpu,
+        "predraw": {"ms": predraw_ms, "roots": GB, "search_kernel_ms": kern_ms, "ratio_to_search": predraw_ms / kern_ms,
+                    "what": "host set-up, outside the timed region: the reference-order draws of all global roots "
+                            "(Dirichlet(0.25) noise, first-tie choice, action uniform; MCTS/mcts.py:57-66,149, "
+                            "MCTS/node.py:86, MCTS/mcts.py:118-120) on NumPy's legacy MT19937 stream by "
+                            "rng.predraw (libmzh mzh_rng_predraw), bit-identical to the NumPy calls"},
         "dist": dinfo,
         "build_id": _lib.build_id(),
     }
@@ -616,6 +676,29 @@ def main():
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def dry_run(a, world, rank, GB, S, N):
+    """--dry-run: the ranks and the process group, no GPU (rank 0 prints the line's rank fields)"""
+    from muzero_hanoi_amd import distributed as mdist
+
+    shards = [mdist.shard_range(GB, world, r) for r in range(world)]
+    dinfo = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group(a.dist_backend)
+        mine = torch.tensor([float(rank), float(shards[rank][1] - shards[rank][0])], dtype=torch.float64)
+        allr = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+        dist.all_gather(allr, mine)
+        dinfo = {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()),
+                 "ranks": [int(x[0]) for x in allr], "roots_per_rank": [int(x[1]) for x in allr]}
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                          "config": {"baseline_config": a.config, "n_disks": N, "sims_per_move": S,
+                                     "global_roots": GB, "shards": shards},
+                          "dist": dinfo}), flush=True)
 
 
 if __name__ == "__main__":

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MZH_ABI_VERSION 3
+#define MZH_ABI_VERSION 4
 
 #define MZH_OK 0
 #define MZH_ERR_ARG (-1)         /* bad argument / shape (ValueError in Python)              */
@@ -165,7 +165,8 @@ typedef struct mzh_search_args {
    * exponent (integer exponents are exact products); without it the device pow is used, which can
    * differ from NumPy's vectorised pow in the last bit. */
   const double* pow_table;
-  /* HOST pointer (nullable): filled with the plan of the launched instantiation (below) */
+  /* HOST pointer (nullable): filled with the plan of the launched instantiation (below); B = 0
+   * launches nothing and reports kernel "none" */
   struct mzh_search_plan* plan_out;
 } mzh_search_args;
 
@@ -190,6 +191,24 @@ int mzh_search_replay(mzh_engine* eng, const mzh_search_args* args, mzh_stream s
  * arguments (has_minmax_in: args.minmax_in != NULL).  Host-only: needs no device and no engine. */
 int mzh_search_plan_query(int support, int B, int n_sims, uint32_t flags, int replay, int has_minmax_in,
                           mzh_search_plan* out);
+
+/* ---------------------------------------------------------------------------------------------
+ * Reference-order host pre-draw (HOST pointers only; no device, no engine).  Replaces the NumPy
+ * calls B sequential run_mcts calls make on the global legacy stream, in their order per call:
+ *   np.random.dirichlet(np.ones_like(prob) * alpha)   MCTS/mcts.py:57-66,148-149  (k > 0)
+ *   np.random.choice(<n_tie tied indices>)            MCTS/node.py:86             (n_tie > 1 draws)
+ *   np.random.choice(np.arange(6), p=pi)              MCTS/mcts.py:118-120        (draw_action: the
+ *                                                     one random_sample() it consumes)
+ * NumPy's legacy RandomState algorithms (csrc/mzh_rng.cpp) on NumPy's own MT19937 state:
+ *   mt_state    in/out  numpy mt19937_state {uint32 key[624]; int pos} (the bit generator's
+ *                       ctypes.state_address), advanced in place exactly as NumPy would
+ *   gauss_state in/out  {has_gauss, cached deviate} of the RandomState (read only for alpha > 1)
+ *   alpha [k]           Dirichlet parameters as float64 (each > 0, else MZH_ERR_ARG as NumPy's
+ *                       ValueError('alpha <= 0'))
+ *   noise [B][k], tie [B] (index into the tied set), action_u [B]: outputs.
+ * MZH_ERR_ARG for a bad argument, before anything is drawn. */
+int mzh_rng_predraw(void* mt_state, double* gauss_state, int B, int k, const double* alpha, int n_tie,
+                    int draw_action, double* noise, int32_t* tie, double* action_u);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused training update.  Replaces Muzero._update (Muzero.py:209-274: represent, U unrolled

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "libmzh.so")
 LIB_PATH = os.environ.get("MZH_LIB") or DEFAULT_LIB  # MZH_LIB: diagnostic builds
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MZH_OK = 0
 MZH_ERR_ARG = -1
 MZH_ERR_HIP = -2
@@ -88,6 +88,8 @@ SIGNATURES = {
     "mzh_search_replay": (ctypes.c_int, [_vp, ctypes.POINTER(SearchArgs), _vp]),
     "mzh_search_plan_query": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
                                              ctypes.c_int, ctypes.POINTER(SearchPlan)]),
+    "mzh_rng_predraw": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int,
+                                       _vp, _vp, _vp]),
     "mzh_train_scratch_bytes": (ctypes.c_int, [ctypes.c_int] * 4 + [ctypes.POINTER(ctypes.c_size_t)]),
     "mzh_train_transpose": (ctypes.c_int, [ctypes.POINTER(TrainArgs), _vp]),
     "mzh_train_update": (ctypes.c_int, [ctypes.POINTER(TrainArgs), _vp]),

@@ -17,6 +17,10 @@ REPO = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libmzh.so")
 OBJ = os.path.join(HERE, "_obj")
 SOURCES = ["mzh_api.hip", "mzh_search.hip", "mzh_wave.hip", "mzh_env.hip", "mzh_train.hip"]
+# host-only sources, compiled by g++ like the NumPy C code they restate (no -march: no FMA; see
+# csrc/mzh_rng.cpp)
+HOST_SOURCES = ["mzh_rng.cpp"]
+HOST_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MZH_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off",
@@ -27,8 +31,8 @@ BUILD_ID_MARKER = b"MZH_BUILD_ID:"
 
 
 def source_files():
-    """every file the library is compiled from: csrc/*.hip, csrc/*.h and include/mzh.h"""
-    fs = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".h")))
+    """every file the library is compiled from: csrc/*.hip, csrc/*.cpp, csrc/*.h and include/mzh.h"""
+    fs = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp", ".h")))
     return [os.path.join(CSRC, f) for f in fs] + [os.path.join(REPO, "include", "mzh.h")]
 
 
@@ -42,6 +46,7 @@ def source_hash(flags=None):
         h.update(b"\0")
     # flags without the checkout's absolute path (the GPU box runs the same tree from another path)
     h.update(" ".join(FLAGS if flags is None else flags).replace(REPO, "<repo>").encode())
+    h.update(" ".join(HOST_FLAGS).encode())
     return h.hexdigest()[:20]
 
 
@@ -89,6 +94,11 @@ def build(verbose=False, force=False, diag=False, tag="", defines=()):
         o = os.path.join(obj_dir, src.replace(".hip", ".o"))
         if force or _stale(o, [s] + headers):
             jobs.append([HIPCC, *flags, "-c", s, "-o", o])
+    for src in HOST_SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(obj_dir, src.replace(".cpp", ".host.o"))
+        if force or _stale(o, [s] + headers):
+            jobs.append(["g++", *HOST_FLAGS, "-I", os.path.join(REPO, "include"), "-c", s, "-o", o])
 
     def run(cmd):
         if verbose:
@@ -103,6 +113,7 @@ def build(verbose=False, force=False, diag=False, tag="", defines=()):
             if verbose and err:
                 print(err, file=sys.stderr)
     objs = [os.path.join(obj_dir, s.replace(".hip", ".o")) for s in SOURCES]
+    objs += [os.path.join(obj_dir, s.replace(".cpp", ".host.o")) for s in HOST_SOURCES]
     if force or jobs or _stale(lib_path, objs):
         # provenance: the build id as a host-only object linked into the library (mzh_build_id())
         id_src = os.path.join(obj_dir, "mzh_build_id.cpp")
@@ -112,7 +123,7 @@ def build(verbose=False, force=False, diag=False, tag="", defines=()):
         id_obj = os.path.join(obj_dir, "mzh_build_id.o")
         run(["g++", "-O2", "-fPIC", "-c", id_src, "-o", id_obj])
         run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, id_obj, "-o", lib_path,
-             "-Wl,-rpath,/opt/rocm/lib"])
+             "-Wl,-rpath,/opt/rocm/lib", "-lm"])
     with open(stamp, "w") as f:
         f.write(want)
     with open(lib_path + ".flags", "w") as f:  # what this .so was built with (A/B logs cite it)

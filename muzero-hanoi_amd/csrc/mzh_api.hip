@@ -549,7 +549,13 @@ static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream s
   if (a->n_sims > eng->max_sims) return fail(MZH_ERR_CAPACITY, "n_sims=%d > max_sims=%d", a->n_sims, eng->max_sims);
   if (!(a->temperature >= 0.0 && a->temperature <= 1.0))
     return fail(MZH_ERR_TEMPERATURE, "Expect `temperature` to be in the range [0.0, 1.0], got %g", a->temperature);
-  if (a->B == 0) return MZH_OK;
+  if (a->B == 0) {  // nothing launches: the plan says so (a caller naming the kernel sees "none")
+    if (a->plan_out) {
+      memset(a->plan_out, 0, sizeof(*a->plan_out));
+      snprintf(a->plan_out->kernel, sizeof(a->plan_out->kernel), "none");
+    }
+    return MZH_OK;
+  }
   if (!a->visits) return fail(MZH_ERR_ARG, "visits output is required");
   if (replay) {
     if (!a->rp_root_pi || (a->n_sims > 0 && !a->rp_sim))

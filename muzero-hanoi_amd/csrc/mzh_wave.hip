@@ -713,7 +713,6 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
     float r32[NT], v32[NT];
     mzw_chain<NT, 4, NOV, false, SUP33, 8>(net.rwd, rw, hx, noh, rl, lane, r32, wst, net.pol.soff);  // reward from h' (networks.py:132-135)
     mzw_bias2<NT, NOV>(net.rwd, rw, rl, g);
-#pragma unroll
     MZH_STAMP(6);
 #pragma unroll
     for (int n = 0; n < NT; ++n) rew[n] = mzw_head<NT, NOV>(rl, n, lane, SUP33 ? r32[n] : 0.0f, net.rwd.b32);

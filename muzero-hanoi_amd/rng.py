@@ -12,10 +12,18 @@ kernel:
                                                                U = 0, Q = 0; README.md:49)
                [u_r      = random_sample()]                    if stochastic: choice(6, p=pi)
 
+`predraw` makes those draws with libmzh's host restatement of NumPy's legacy algorithms
+(`mzh_rng_predraw`, csrc/mzh_rng.cpp) on the RandomState's own MT19937 state, advanced in place
+through the bit generator's ctypes interface: the same arrays and the same stream position as the
+NumPy calls (`predraw_numpy`, kept as the specification and for RandomStates over another bit
+generator), at C speed (65,536 roots: ~30 ms instead of ~1.3 s).
+
 Any further tie the kernel meets is counted in `extra_ties` (none was observed in the
 reference traces, tests/golden/rng_order.json); when it is non-zero the RNG streams of the two
 implementations have diverged and the caller is told so.
 """
+import ctypes
+
 import numpy as np
 
 
@@ -23,15 +31,18 @@ def uses_noise(deterministic, alpha, eps):
     return (not deterministic) and alpha > 0.0 and eps > 0.0
 
 
-def predraw(n_roots, *, deterministic, alpha, eps=0.25, rng=None, draw_action=True):
-    """Draw (noise[B,6] f64 | None, tie[B] i32, u[B] f64 | None) from `rng` (default: the
-    global legacy NumPy stream, exactly as the reference consumes it).  draw_action=False: a
-    search that raises before its action draw (invalid temperature, mcts.py:113,163-166)."""
+def _alphas(alpha):
+    """np.ones_like(prob) * alpha with prob float32 (mcts.py:148): float32 parameters"""
+    return np.ones(6, np.float32) * alpha
+
+
+def predraw_numpy(n_roots, *, deterministic, alpha, eps=0.25, rng=None, draw_action=True):
+    """The reference's NumPy calls, one root at a time (the specification `predraw` restates)."""
     rs = np.random if rng is None else rng
     noise = np.empty((n_roots, 6), np.float64) if uses_noise(deterministic, alpha, eps) else None
     tie = np.empty(n_roots, np.int32)
     u = None if (deterministic or not draw_action) else np.empty(n_roots, np.float64)
-    alphas = np.ones(6, np.float32) * alpha  # np.ones_like(prob) * alpha with prob float32
+    alphas = _alphas(alpha)
     cand = np.arange(6)
     for r in range(n_roots):
         if noise is not None:
@@ -42,8 +53,76 @@ def predraw(n_roots, *, deterministic, alpha, eps=0.25, rng=None, draw_action=Tr
     return noise, tie, u
 
 
+def _random_state(rng):
+    rs = np.random.mtrand._rand if rng is None or rng is np.random else rng
+    if not isinstance(rs, np.random.RandomState):
+        raise TypeError(f"predraw needs a legacy numpy.random.RandomState (the reference's stream), got {type(rs)}")
+    return rs
+
+
+_CHECKED = False
+
+
+def _self_check():
+    """Once per process: the C restatement against NumPy on a private RandomState (a NumPy whose
+    MT19937 state layout or legacy algorithms differed would fail here, loudly)."""
+    global _CHECKED
+    if _CHECKED:
+        return
+    for alpha, det in ((0.25, False), (2.5, False), (0.25, True)):
+        a, b = np.random.RandomState(20261018), np.random.RandomState(20261018)
+        got = _predraw_c(a, 16, deterministic=det, alpha=alpha, eps=0.25, draw_action=True)
+        want = predraw_numpy(16, deterministic=det, alpha=alpha, rng=b)
+        sa, sb = a.get_state(), b.get_state()
+        same = all((x is None and y is None) or np.array_equal(x, y) for x, y in zip(got, want))
+        if not (same and np.array_equal(sa[1], sb[1]) and sa[2:] == sb[2:]):
+            raise RuntimeError("mzh_rng_predraw disagrees with this NumPy's legacy RandomState draws")
+    _CHECKED = True
+
+
+def _predraw_c(rs, n_roots, *, deterministic, alpha, eps, draw_action):
+    from . import _lib
+
+    L = _lib.lib()
+    noisy = uses_noise(deterministic, alpha, eps)
+    alphas = _alphas(alpha).astype(np.float64)
+    if noisy and not (alphas > 0).all():
+        raise ValueError("alpha <= 0")  # RandomState.dirichlet (alpha underflows in float32)
+    noise = np.empty((n_roots, 6), np.float64) if noisy else None
+    tie = np.empty(n_roots, np.int32)
+    u = np.empty(n_roots, np.float64) if (not deterministic and draw_action) else None
+    # the gamma sampler uses the polar Gaussian (and the RandomState's cached deviate) only for alpha > 1
+    gauss_used = noisy and float(alphas[0]) > 1.0
+    if gauss_used:
+        st = rs.get_state()
+        g = np.array([float(st[3]), st[4]], np.float64)
+    else:
+        g = np.zeros(2, np.float64)
+    addr = rs._bit_generator.ctypes.state_address
+    p = lambda x: None if x is None else x.ctypes.data_as(ctypes.c_void_p)
+    status = L.mzh_rng_predraw(ctypes.c_void_p(addr), p(g), int(n_roots), 6 if noisy else 0, p(alphas), 6,
+                               1 if u is not None else 0, p(noise), p(tie), p(u))
+    _lib.check(status, "mzh_rng_predraw")
+    if gauss_used:
+        st = rs.get_state()  # the key / pos the C code advanced in place, with the new Gaussian cache
+        rs.set_state((st[0], st[1], st[2], int(g[0]), float(g[1])))
+    return noise, tie, u
+
+
+def predraw(n_roots, *, deterministic, alpha, eps=0.25, rng=None, draw_action=True):
+    """Draw (noise[B,6] f64 | None, tie[B] i32, u[B] f64 | None) from `rng` (default: the global
+    legacy NumPy stream), exactly as B sequential run_mcts calls consume it.  draw_action=False: a
+    search that raises before its action draw (invalid temperature, mcts.py:113,163-166)."""
+    rs = _random_state(rng)
+    if type(rs._bit_generator).__name__ != "MT19937":
+        return predraw_numpy(n_roots, deterministic=deterministic, alpha=alpha, eps=eps, rng=rs,
+                             draw_action=draw_action)
+    _self_check()
+    return _predraw_c(rs, n_roots, deterministic=deterministic, alpha=alpha, eps=eps, draw_action=draw_action)
+
+
 def synthetic_draws(n_roots, *, deterministic, alpha, eps=0.25, seed=0):
-    """Vectorised draws of the same distributions for large synthetic batches (bench).
+    """Vectorised draws of the same distributions for large synthetic batches.
     Not stream-compatible with the legacy global RNG; used where no parity claim is made."""
     g = np.random.default_rng(seed)
     noise = None

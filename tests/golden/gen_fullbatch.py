@@ -1,0 +1,123 @@
+"""Whole-batch oracle outputs for the BASELINE.json search configs at their full per-GPU sizes,
+on the exact inputs bench.py searches (seed 0): the GPU test (tests/test_gpu_parity.py::
+test_search_full_batch_equals_oracle) compares EVERY root of the HIP search with these.
+
+    python tests/golden/gen_fullbatch.py [TAG ...]        # ~10 min on 8 host cores
+
+Inputs, as bench.py builds them (bench.random_roots + rng.predraw on RandomState(seed), global
+root order, then the rank's contiguous shard); weights tests/golden/weights_N{n}_s0.npz (the
+reference's MuZeroNet(TD_return=True) after torch.manual_seed(0), identical to bench.py's
+random-init network -- checked below).  The outputs come from the C oracle (oracle/mzh_oracle.c,
+pinned on the reference's own fixtures), run one process per host core over root chunks (roots are
+independent: each has its own fresh MinMaxStats, MCTS/mcts.py:23).
+
+Stored per config (np.savez_compressed): visits uint8 [B,6], action uint8 [B], sel_steps uint16 [B],
+extra_ties uint8 [B]; root Q and the (max, min) MinMaxStats as SHA-256 digests of 256-root blocks
+of their float64 bytes (rootq_minmax_sha [B/256, 32] uint8) -- exact, 1/64 the size -- and for the
+4,096-root config the float64 arrays themselves; inputs_sha: digest of the regenerated inputs.
+"""
+import hashlib
+import multiprocessing as mp
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+# tag: (disks, global roots, sims, world, rank) -- BASELINE.json configs[1..4] as bench.py runs them
+CONFIGS = {
+    "c1_4096": (4, 4096, 50, 1, 0),          # configs[1]
+    "c3_16384": (4, 16384, 200, 1, 0),       # configs[3]
+    "c2_65536": (4, 65536, 50, 1, 0),        # configs[2], the metric's batch on one GPU
+    "c4_shard0of8": (7, 262144, 100, 8, 0),  # configs[4], rank 0's 32,768-root shard at N=8
+}
+SEED = 0
+BLOCK = 256
+
+
+def inputs(tag):
+    """(obs f32 [B,3N], noise f64 [B,6], tie i32 [B], u f64 [B]) exactly as bench.py makes them"""
+    import bench
+    from muzero_hanoi_amd import distributed as mdist
+    from muzero_hanoi_amd import rng
+
+    n, GB, S, W, r = CONFIGS[tag]
+    obs = bench.random_roots(n, GB, SEED)
+    noise, tie, u = rng.predraw(GB, deterministic=False, alpha=0.25, rng=np.random.RandomState(SEED))
+    return tuple(np.ascontiguousarray(mdist.shard(x, W, r)) for x in (obs, noise, tie, u))
+
+
+def inputs_sha(obs, noise, tie, u):
+    h = hashlib.sha256()
+    for x in (obs.astype(np.float32), noise.astype(np.float64), tie.astype(np.int32), u.astype(np.float64)):
+        h.update(np.ascontiguousarray(x).tobytes())
+    return np.frombuffer(h.digest(), np.uint8)
+
+
+def block_sha(root_q, mm):
+    """SHA-256 of each 256-root block's float64 root Q then (max, min) bytes"""
+    B = len(root_q)
+    out = np.zeros((-(-B // BLOCK), 32), np.uint8)
+    for k in range(out.shape[0]):
+        sl = slice(k * BLOCK, min(B, (k + 1) * BLOCK))
+        h = hashlib.sha256(np.ascontiguousarray(root_q[sl], np.float64).tobytes())
+        h.update(np.ascontiguousarray(mm[sl], np.float64).tobytes())
+        out[k] = np.frombuffer(h.digest(), np.uint8)
+    return out
+
+
+def weights(n):
+    from oracle import oracle
+
+    w, in_dim, sup = oracle.load_weights_npz(os.path.join(HERE, f"weights_N{n}_s0.npz"))
+    return oracle.flat_weights(w), sup
+
+
+def _chunk(args):
+    n, S, obs, noise, tie, u = args
+    from oracle import oracle
+
+    flat, sup = weights(n)
+    r = oracle.search(n, S, obs, flat=flat, support=sup, noise=noise, tie_idx=tie, action_u=u, temperature=1.0,
+                      deterministic=False, discount=0.8)
+    return {k: r[k] for k in ("visits", "rootQ", "mm_max", "mm_min", "action", "sel_steps", "extra_ties")}
+
+
+def generate(tag, procs):
+    import torch
+
+    n, GB, S, W, r = CONFIGS[tag]
+    obs, noise, tie, u = inputs(tag)
+    B = len(obs)
+    # bench.py's network is MuZeroNet after torch.manual_seed(0): the same weights as the fixture
+    from muzero_hanoi_amd import engine
+    from muzero_hanoi_amd.networks import MuZeroNet
+
+    torch.manual_seed(SEED)
+    net = MuZeroNet(3 * n, 6, 0.002, "cpu", TD_return=True)
+    assert np.array_equal(engine.flat_weights(net.state_dict()), weights(n)[0]), "bench weights != fixture weights"
+    step = 512
+    jobs = [(n, S, obs[i:i + step], noise[i:i + step], tie[i:i + step], u[i:i + step]) for i in range(0, B, step)]
+    with mp.get_context("spawn").Pool(procs) as pool:
+        parts = pool.map(_chunk, jobs)
+    cat = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+    mm = np.stack([cat["mm_max"], cat["mm_min"]], 1)
+    assert cat["sel_steps"].max() < 65536 and cat["visits"].max() < 256
+    out = dict(n_disks=n, n_sims=S, global_roots=GB, world=W, rank=r, seed=SEED,
+               visits=cat["visits"].astype(np.uint8), action=cat["action"].astype(np.uint8),
+               sel_steps=cat["sel_steps"].astype(np.uint16), extra_ties=cat["extra_ties"].astype(np.uint8),
+               rootq_minmax_sha=block_sha(cat["rootQ"], mm), inputs_sha=inputs_sha(obs, noise, tie, u))
+    if B <= 4096:
+        out.update(root_q=cat["rootQ"], minmax=mm)
+    np.savez_compressed(os.path.join(HERE, f"full_{tag}.npz"), **out)
+    print(tag, B, "roots:", "visits sum ok" if (cat["visits"].sum(1) == S).all() else "BAD", flush=True)
+
+
+if __name__ == "__main__":
+    tags = sys.argv[1:] or list(CONFIGS)
+    procs = min(8, os.cpu_count() or 1)
+    for t in tags:
+        generate(t, procs)

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol(lib):
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(lib.SIGNATURES), "ctypes signature table out of sync with include/mzh.h"
-    assert L.mzh_abi_version() == lib.ABI_VERSION == 3
+    assert L.mzh_abi_version() == lib.ABI_VERSION == 4
 
 
 def _c_offsets(struct, fields, tmp_path):

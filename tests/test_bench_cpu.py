@@ -137,3 +137,46 @@ def test_traffic_summary_keeps_the_bench_instantiation(tmp_path):
     assert out["fused"]["FETCH_SIZE"] == 100.0 and out["fused"]["hbm_read_bytes_corrected"] == 100.0 * 1024 * 2
     assert out["tree"]["kernel"] == full(tree_k) and out["tree"]["FETCH_SIZE"] == 10.0
     assert list(out["other"]) == [full(other_k)]
+
+
+def _bench_env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def test_gpus_n_without_launcher_starts_n_ranks():
+    """`python bench.py --gpus 2` with no launcher must not print a 1-GPU line: it starts
+    torch.distributed.run with 2 ranks itself (gloo, --dry-run: the rank plumbing without a GPU)"""
+    import subprocess
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--dry-run"], capture_output=True, text=True, timeout=300, env=_bench_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["dist"]["world_size"] == 2 and rec["dist"]["backend"] == "gloo"
+    assert sorted(rec["dist"]["ranks"]) == [0, 1] and sum(rec["dist"]["roots_per_rank"]) == 65536
+
+
+def test_gpus_mismatch_with_launcher_world_fails():
+    """a launcher's WORLD_SIZE that differs from --gpus is an error, never a mislabelled line"""
+    import subprocess
+
+    env = _bench_env()
+    env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert r.returncode != 0 and "WORLD_SIZE" in (r.stderr + r.stdout)
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_empty_shard_is_rejected():
+    """more ranks than roots: a clear error, not a crash on an empty launch"""
+    import subprocess
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--roots-per-gpu", "0", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=_bench_env(), cwd=ROOT)
+    assert r.returncode != 0 and "non-empty shard" in (r.stderr + r.stdout)

@@ -1,4 +1,4 @@
-# round-4 final pass, part 1: GPU tests + smoke on the final build, the driver's default bench command (with
+# final pass of a round: GPU tests + smoke on the final build, the driver's default bench command (with
 # the CPU baseline), a 2-rank gloo rehearsal of the N>1 bench path on one GPU
 set -e
 mkdir -p gpurun_out

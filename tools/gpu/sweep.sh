@@ -1,7 +1,7 @@
-# round 4 profile sweep: for each bench workload the un-profiled bench line, rocprofv3 --kernel-trace --stats
+# profile sweep: for each bench workload the un-profiled bench line, rocprofv3 --kernel-trace --stats
 # and separate PMC passes (tools/prof.sh), summarised and recorded under the profiled run's own key
 # (tools/traffic.py), then the bench line re-run with the recorded traffic.
-#   bash tools/gpu/r04_sweep.sh "c2:" "b8192:--config 2 --shard 0/8" ...      (TAG:BENCH_ARGS pairs)
+#   bash tools/gpu/sweep.sh "c2:" "b8192:--config 2 --shard 0/8" ...      (TAG:BENCH_ARGS pairs)
 set -e
 mkdir -p gpurun_out
 for spec in "$@"; do
