@@ -508,3 +508,49 @@ def test_search_caller_bounds_instantiation(mzh, oracle, B, tile):
     assert np.array_equal(o2["visits"][idx], ref["visits"])
     assert np.array_equal(o2["root_q"][idx], ref["rootQ"])
     assert np.array_equal(o2["minmax"][idx, 0], ref["mm_max"]) and np.array_equal(o2["minmax"][idx, 1], ref["mm_min"])
+
+
+# ------------------------------------------------- whole-batch oracle parity at BASELINE sizes
+FULL_BATCH = ["c1_4096", "c3_16384", "c2_65536", "c4_shard0of8"]
+
+
+def _first_diff(a, b):
+    bad = np.flatnonzero(~(np.asarray(a) == np.asarray(b)).reshape(len(a), -1).all(1))
+    return None if bad.size == 0 else (int(bad[0]), int(bad.size))
+
+
+@pytest.mark.parametrize("tag", FULL_BATCH)
+def test_search_full_batch_equals_oracle(mzh, tag):
+    """EVERY root of each BASELINE.json search config at its full per-GPU size (configs[1] 4,096
+    roots; configs[3] 16,384 x 200 sims; configs[2] 65,536 roots on one GPU; configs[4]'s rank-0
+    shard at N=8, 32,768 7-disk roots x 100 sims), on bench.py's own inputs and reference-order
+    draws, through the kernel the library picks, equals the C oracle's whole-batch outputs
+    (tests/golden/gen_fullbatch.py; MCTS/mcts.py:34-126): visits, action, selection steps and extra
+    ties root by root, root Q and MinMaxStats bit for bit through per-256-root SHA-256 digests."""
+    import sys
+
+    sys.path.insert(0, GOLDEN)
+    import gen_fullbatch as gf
+
+    z = golden(f"full_{tag}.npz")
+    n, S = int(z["n_disks"]), int(z["n_sims"])
+    obs, noise, tie, u = gf.inputs(tag)
+    assert np.array_equal(gf.inputs_sha(obs, noise, tie, u), z["inputs_sha"]), "regenerated inputs differ"
+    flat, sup = gf.weights(n)
+    B = len(obs)
+    eng = _engine(mzh, n, S, B, sup, flat)
+    tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
+    o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0,
+                   deterministic=False, discount=0.8, eps=0.25)
+    kern = o["_plan"]["kernel"]
+    o = {k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")}
+    eng.close()
+    for k, want in (("visits", z["visits"]), ("action", z["action"]), ("sel_steps", z["sel_steps"]),
+                    ("extra_ties", z["extra_ties"])):
+        d = _first_diff(o[k].astype(np.int64), want.astype(np.int64))
+        assert d is None, f"{tag} ({kern}): {k} differs at root {d[0]} ({d[1]} of {B} roots)"
+    sha = gf.block_sha(o["root_q"], o["minmax"])
+    d = _first_diff(sha, z["rootq_minmax_sha"])
+    assert d is None, f"{tag} ({kern}): root Q / MinMaxStats differ in 256-root block {d[0]} ({d[1]} blocks)"
+    if "root_q" in z:
+        assert np.array_equal(o["root_q"], z["root_q"]) and np.array_equal(o["minmax"], z["minmax"])
