@@ -98,7 +98,7 @@ def parse():
     p.add_argument("--no-tree", action="store_true", help="skip the live select/backup (replay) measurement")
     p.add_argument("--no-minmax-leg", action="store_true",
                    help="skip timing the instantiation searches with caller MinMaxStats bounds run (training / acting)")
-    p.add_argument("--kernel", choices=["auto", "coop", "wave", "wave16"], default="auto")
+    p.add_argument("--kernel", choices=["auto", "coop", "occ2", "wave", "wave16"], default="auto")
     p.add_argument("--tile", type=int, choices=[16, 32], default=None,
                    help="cooperative kernel: roots per workgroup (default by batch size)")
     p.add_argument("--dist-backend", default="nccl",

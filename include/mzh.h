@@ -47,6 +47,8 @@ extern "C" {
 #define MZH_FLAG_KERNEL_WAVE16 8u /* force the wave-independent kernel, 16 roots per wave (default for 8192 < B < 53248) */
 #define MZH_FLAG_COOP_TILE16 16u /* cooperative kernel: 16 roots per workgroup (default for B <= 4096) */
 #define MZH_FLAG_COOP_TILE32 32u /* cooperative kernel: 32 roots per workgroup (default for B > 4096) */
+#define MZH_FLAG_COOP_OCC2 64u /* cooperative kernel, 16-root tiles, two workgroups per CU
+                                  (mzh_search_occ2_kernel; MLP searches whose LDS fits twice per CU) */
 
 typedef struct mzh_engine mzh_engine;
 typedef void* mzh_stream; /* hipStream_t */

@@ -27,6 +27,7 @@ MZH_FLAG_KERNEL_WAVE = 4  # wave-independent kernel (mzh_wave.hip), 32 roots per
 MZH_FLAG_KERNEL_WAVE16 = 8  # wave-independent kernel, 16 roots per wave
 MZH_FLAG_COOP_TILE16 = 16  # cooperative kernel, 16 roots per workgroup
 MZH_FLAG_COOP_TILE32 = 32  # cooperative kernel, 32 roots per workgroup
+MZH_FLAG_COOP_OCC2 = 64  # cooperative kernel, 16-root tiles, two workgroups per CU (mzh_search_occ2_kernel)
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32

@@ -498,6 +498,16 @@ static int make_plan(int B, int S, uint32_t flags, bool replay, int support, boo
     q.mmin = 0;  // the wave kernel decides the exact normaliser per selection
   } else {
     q.R = pick_tile(B, flags);
+    // the two-workgroups-per-CU 16-root kernel: forced by MZH_FLAG_COOP_OCC2 (MLP searches; its LDS must
+    // leave room for the second workgroup)
+    if ((flags & MZH_FLAG_COOP_OCC2) && !replay && 2 * mzh_search_smem_bytes(16, S, false, true) <= kMaxLds) {
+      q.R = 16;
+      q.occ2 = 1;
+      q.ohl = 0;
+      q.sup33 = support == 33;
+      *pl = q;
+      return MZH_OK;
+    }
     if (mzh_search_smem_bytes(q.R, S, false) > kMaxLds) q.R = 16;
     if (mzh_search_smem_bytes(q.R, S, false) > kMaxLds)
       return fail(MZH_ERR_CAPACITY, "n_sims=%d exceeds the LDS path budget", S);
@@ -519,6 +529,12 @@ static void plan_info(const MzhSearchPlan& q, int B, int S, mzh_search_plan* out
     out->roots_per_workgroup = 4 * 16 * q.nt;
     out->smem_bytes = (int64_t)mzh_wave_smem_bytes(S, q.nt);
     snprintf(out->kernel, sizeof(out->kernel), "mzh_wave_kernel<%d, %s, %s>", q.nt, tf[q.replay], tf[q.sup33]);
+  } else if (q.occ2) {
+    out->roots_per_wave = 4;
+    out->threads_per_workgroup = MZH_THREADS;
+    out->roots_per_workgroup = 16;
+    out->smem_bytes = (int64_t)mzh_search_smem_bytes(16, S, false, true);
+    snprintf(out->kernel, sizeof(out->kernel), "mzh_search_occ2_kernel<%s, %s>", tf[q.sup33], tf[q.mmin]);
   } else {
     out->roots_per_wave = q.R / 4;
     out->threads_per_workgroup = MZH_THREADS;

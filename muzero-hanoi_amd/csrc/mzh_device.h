@@ -532,11 +532,16 @@ struct MzhNoMid {
 // MID (optional): independent VALU / LDS work, mid(kb) placed in the region of k-block kb's MFMAs, so
 // it issues under their execution instead of on the phase's critical path (the latent normalisation
 // beside rwd0; it must neither read this chain's output nor write its A operand or its LDS output)
-template <int MT, int NJ, int KB, bool ALL = false, int PT = 0, int PNB = 0, bool NAT = false, class MID = MzhNoMid>
+// K-split chains (8-fragment chunks, mzh_mlp_recurrent_c8): KOFF = the chunk's first k-block of the
+// layer (its A operand is read from there on); ACCIN: the chain continues from accio (the previous
+// chunk's partial accumulators -- the same k-ordered fp32 FMA chain, only split across two calls);
+// EPI = false: no epilogue, the partial accumulators are left in accio.
+template <int MT, int NJ, int KB, bool ALL = false, int PT = 0, int PNB = 0, bool NAT = false, class MID = MzhNoMid,
+          int KOFF = 0, bool ACCIN = false, bool EPI = true>
 __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhChunk& c, const float* A, int lda,
                                               bool relu, const float* oht, const int* act, int lane,
                                               const MzhChunk* pc = nullptr, const floatx4* areg = nullptr,
-                                              MID mid = MID{}) {
+                                              MID mid = MID{}, floatx4* accio = nullptr) {
   // areg (optional): the A operand of all KB k-blocks already in registers, [kb * MT + m] (chunks
   // of one phase that share A load it once)
   static_assert(PT <= 16 && PNB <= 4, "ring chunk too large");
@@ -551,12 +556,12 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
 #pragma unroll
   for (int q = 0; q < NJ; ++q)
 #pragma unroll
-    for (int m = 0; m < MT; ++m) acc[q][m] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int m = 0; m < MT; ++m) acc[q][m] = ACCIN ? accio[q * MT + m] : floatx4{0.f, 0.f, 0.f, 0.f};
   // A operands double-buffered one k-block ahead: block kb + 1's LDS reads are issued before block
   // kb's MFMAs (pinned by the scheduling barrier), so a K = 256 chain does not wait on LDS latency
   // between its MFMAs
   floatx4 a[2][MT];  // [buffer][row tile]: k-steps j = 0..3 of one k-block (A in k-block order)
-  const float* arow = A + r * lda + 4 * g;
+  const float* arow = A + r * lda + 4 * g + 16 * KOFF;
   if (!areg) {
 #pragma unroll
     for (int m = 0; m < MT; ++m) a[0][m] = *reinterpret_cast<const floatx4*>(arow + m * 16 * lda);
@@ -637,9 +642,15 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
               acc[q][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(aop(kb, m)[j], f[fs(q, kb)][j], acc[q][m], 0, 0, 0);
         }
         if (fs(q, kb) < PT) refill(fs(q, kb));
-        epilogue(q);
+        if (EPI) epilogue(q);
       }
     }
+  }
+  if (!EPI) {
+#pragma unroll
+    for (int q = 0; q < NJ; ++q)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) accio[q * MT + m] = acc[q][m];
   }
 #pragma unroll
   for (int q = 0; q < PNB; ++q) bv[q] = mzh_ld1(prs, 4 * (lane & 15), pc->boff[q]);
@@ -1150,6 +1161,146 @@ __device__ __forceinline__ void mzh_mlp_recurrent_body(SM& sm, const MzhNet& net
     bar();
   }
   MZH_STAMP(12);
+}
+
+// ------------------------------------------------------------------------------------------
+// The same recurrent MLP for a 16-root tile whose workgroup shares its CU with a second one (the
+// two-workgroups-per-CU cooperative kernel, mzh_search_occ2_kernel): <= 256 registers a lane, so the
+// weight ring is two buffers of 8 fragments (fa8, fb8) instead of 16, and every 16-fragment chunk
+// of mzh_mlp_recurrent_body is two 8-fragment chunks -- K = 64 layers two tiles per chunk, K = 256
+// tiles two k-halves (mzh_mma_store KOFF / ACCIN / EPI: one k-ordered chain split across two calls,
+// the same FMAs in the same order).  Chunk i runs from buffer i % 2 and refills it with chunk i + 2
+// as its MFMAs free the slots; per simulation
+//   A1 A2 | B1 B2 | C1 C2 | D1 .. D5 | E1 E2        (E: the waves with a pol2 / val2 tile)
+// so waves with a head tile run 13 chunks and the others 11: the next simulation's A1 / A2 arrive in
+// the swapped buffers and the caller swaps fa8 / fb8 before the next call (mzh_c8_swap, after the
+// tree phase, when those loads have long completed).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ MzhChunk mzh_chunk_khalf(MzhChunk c) {  // the second k-half of a K = 256 tile
+  c.woff[0] += 8 * 1024;
+  return c;
+}
+
+template <class SM>
+__device__ __forceinline__ void mzh_mlp_fetch12_c8(SM& sm, const MzhNet& net, int wave_in, int lane, floatx4* fa,
+                                                   float* ba, floatx4* fb, float* bb) {
+  const int wave = __builtin_amdgcn_readfirstlane(wave_in);
+  mzh_fetch<2, 4, true>(fa, ba, mzh_chunk(net, net.dyn0, wave * 4, 2, sm.hidP, MZH_LD256), lane);
+  mzh_fetch<2, 4, true>(fb, bb, mzh_chunk(net, net.dyn0, wave * 4 + 2, 2, sm.hidP, MZH_LD256), lane);
+}
+
+__device__ __forceinline__ void mzh_c8_swap(floatx4* fa, float* ba, floatx4* fb, float* bb) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const floatx4 t = fa[i];
+    fa[i] = fb[i];
+    fb[i] = t;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float t = ba[i];
+    ba[i] = bb[i];
+    bb[i] = t;
+  }
+}
+
+template <int N2, class SM>
+__device__ __forceinline__ void mzh_mlp_recurrent_c8(SM& sm, const MzhNet& net, int wave_in, int lane, floatx4* fa,
+                                                     float* ba, floatx4* fb, float* bb, const float* onehot) {
+  constexpr int R = 16, MT = 1;
+  const int tid = threadIdx.x;
+  int wave = __builtin_amdgcn_readfirstlane(wave_in);
+  // opaque to the optimiser: the 13 chunk descriptors below are rebuilt each simulation (a few SALU)
+  // instead of being hoisted out of the simulation loop, where they would stay live in SGPRs across the
+  // tree phase and spill
+  asm volatile("" : "+s"(wave));
+  const bool r2 = wave < N2;
+  const int P1 = r2 ? wave * (N2 + 4) : N2 * (N2 + 4) + (wave - N2) * (N2 + 8);
+  const int P2 = P1 + (r2 ? 0 : 4), P3 = P2 + 4;
+  const bool ht = mzh_has_head_tile<N2>(wave);
+  const MzhChunk cA1 = mzh_chunk(net, net.dyn0, wave * 4, 2, sm.hidP, MZH_LD256);
+  const MzhChunk cA2 = mzh_chunk(net, net.dyn0, wave * 4 + 2, 2, sm.hidP, MZH_LD256);
+  const MzhChunk cB1 = mzh_chunk(net, net.dyn2, wave, 1, sm.hraw, MZH_LD64), cB2 = mzh_chunk_khalf(cB1);
+  const MzhChunk cC1 = mzh_chunk(net, net.rwd0, wave * 4, 2, sm.hidR, MZH_LD256);
+  const MzhChunk cC2 = mzh_chunk(net, net.rwd0, wave * 4 + 2, 2, sm.hidR, MZH_LD256);
+  const MzhChunk cR1 = mzh_chunk(net, net.rwd2, wave, 1, sm.lrwd, MZH_LDSUP), cR2 = mzh_chunk_khalf(cR1);
+  const MzhChunk cD1 = r2 ? cR1 : mzh_pred_tiles<R>(sm, net, P1, 2);
+  const MzhChunk cD2 = r2 ? cR2 : mzh_pred_tiles<R>(sm, net, P1 + 2, 2);
+  const MzhChunk cD3 = mzh_pred_tiles<R>(sm, net, P2, 2), cD4 = mzh_pred_tiles<R>(sm, net, P2 + 2, 2);
+  const MzhChunk cD5 = mzh_pred_tiles<R>(sm, net, P3, N2);
+  const MzhChunk cE1 = mzh_head_chunk<R>(sm, net, wave), cE2 = mzh_chunk_khalf(cE1);
+  floatx4 acc[2];
+  // ---- A: dyn0 + one-hot + bias, relu -> hidP (networks.py:129-131)
+  mzh_mma_store<MT, 2, 4, true, 8, 1>(fa, ba, cA1, sm.x, MZH_LD64, true, onehot, sm.act, lane, &cB1);
+  mzh_mma_store<MT, 2, 4, true, 8, 1>(fb, bb, cA2, sm.x, MZH_LD64, true, onehot, sm.act, lane, &cB2);
+  __syncthreads();
+  // ---- B: dyn2 -> h' (one K = 256 chain in two halves)
+  mzh_mma_store<MT, 1, 8, true, 8, 2, false, MzhNoMid, 0, false, false>(fa, ba, cB1, sm.hidP, MZH_LD256, false, nullptr,
+                                                                      nullptr, lane, &cC1, nullptr, MzhNoMid{}, acc);
+  mzh_mma_store<MT, 1, 8, true, 8, 2, false, MzhNoMid, 8, true, true>(fb, bb, cB2, sm.hidP, MZH_LD256, false, nullptr,
+                                                                     nullptr, lane, &cC2, nullptr, MzhNoMid{}, acc);
+  __syncthreads();
+  // ---- C: rwd0 on h' (networks.py:132), the latent normalisation under its MFMAs
+  MzhNormPass<R> norm;
+  bool slow = false;
+  if (r2) {
+    mzh_mma_store<MT, 2, 4, true, 8, 1>(fa, ba, cC1, sm.hraw, MZH_LD64, true, nullptr, nullptr, lane, &cD1, nullptr,
+                                        [&](int kb) {
+                                          if (kb == 0) norm.load(sm.hraw, tid);
+                                          if (kb == 1) norm.reduce();
+                                          if (kb == 2) slow = norm.template finish<false>(sm.x, tid);
+                                        });
+    mzh_mma_store<MT, 2, 4, true, 8, 1>(fb, bb, cC2, sm.hraw, MZH_LD64, true, nullptr, nullptr, lane, &cD2);
+  } else {
+    mzh_mma_store<MT, 2, 4, true, 8, 2>(fa, ba, cC1, sm.hraw, MZH_LD64, true, nullptr, nullptr, lane, &cD1, nullptr,
+                                        [&](int kb) {
+                                          if (kb == 0) norm.load(sm.hraw, tid);
+                                          if (kb == 1) norm.reduce();
+                                          if (kb == 2) slow = norm.template finish<false>(sm.x, tid);
+                                        });
+    mzh_mma_store<MT, 2, 4, true, 8, 2>(fb, bb, cC2, sm.hraw, MZH_LD64, true, nullptr, nullptr, lane, &cD2);
+  }
+  if (__builtin_expect(slow, 0)) norm.template finish<true>(sm.x, tid);
+  __syncthreads();
+  // ---- D: rwd2 (waves < N2) and the prediction hidden layers (networks.py:140-150) on sm.x
+  {
+    floatx4 ax[4];
+    {
+      const float* arow = sm.x + (lane & 15) * MZH_LD64 + 4 * (lane >> 4);
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) ax[kb] = *reinterpret_cast<const floatx4*>(arow + kb * 16);
+    }
+    if (r2) {
+      mzh_mma_store<MT, 1, 8, true, 8, 2, true, MzhNoMid, 0, false, false>(fa, ba, cD1, sm.hidR, MZH_LD256, false, nullptr,
+                                                                         nullptr, lane, &cD3, nullptr, MzhNoMid{}, acc);
+      mzh_mma_store<MT, 1, 8, true, 8, 2, true, MzhNoMid, 8, true, true>(fb, bb, cD2, sm.hidR, MZH_LD256, false, nullptr,
+                                                                       nullptr, lane, &cD4, nullptr, MzhNoMid{}, acc);
+    } else {
+      mzh_mma_store<MT, 2, 4, true, 8, 2>(fa, ba, cD1, sm.x, MZH_LD64, true, nullptr, nullptr, lane, &cD3, ax);
+      mzh_mma_store<MT, 2, 4, true, 8, 2>(fb, bb, cD2, sm.x, MZH_LD64, true, nullptr, nullptr, lane, &cD4, ax);
+    }
+    // D3 refills its buffer with D5 (N2 tiles); D4 with E1 (head waves) or the next simulation's A1
+    mzh_mma_store<MT, 2, 4, true, 4 * N2, N2>(fa, ba, cD3, sm.x, MZH_LD64, true, nullptr, nullptr, lane, &cD5, ax);
+    if (ht) {
+      mzh_mma_store<MT, 2, 4, true, 8, 1>(fb, bb, cD4, sm.x, MZH_LD64, true, nullptr, nullptr, lane, &cE1, ax);
+      mzh_mma_store<MT, N2, 4, true, 8, 1>(fa, ba, cD5, sm.x, MZH_LD64, true, nullptr, nullptr, lane, &cE2, ax);
+    } else {
+      mzh_mma_store<MT, 2, 4, true, 8, 2>(fb, bb, cD4, sm.x, MZH_LD64, true, nullptr, nullptr, lane, &cA1, ax);
+      mzh_mma_store<MT, N2, 4, true, 8, 2>(fa, ba, cD5, sm.x, MZH_LD64, true, nullptr, nullptr, lane, &cA2, ax);
+    }
+  }
+  __syncthreads();
+  // ---- E: pol2 / val2 (waves with a head tile), bin 32 of the 33-bin heads (the others)
+  if (ht) {
+    float* hin = wave == 0 ? sm.hidP : sm.hidV;
+    mzh_mma_store<MT, 1, 8, true, 8, 2, true, MzhNoMid, 0, false, false>(fb, bb, cE1, hin, MZH_LD256, false, nullptr,
+                                                                       nullptr, lane, &cA1, nullptr, MzhNoMid{}, acc);
+    mzh_mma_store<MT, 1, 8, true, 8, 2, true, MzhNoMid, 8, true, true>(fa, ba, cE2, hin, MZH_LD256, false, nullptr,
+                                                                     nullptr, lane, &cA2, nullptr, MzhNoMid{}, acc);
+  } else if (N2 == 2) {
+    mzh_bin32_wave<R>(sm, net, lane);
+  }
+  __syncthreads();
 }
 
 template <int R>

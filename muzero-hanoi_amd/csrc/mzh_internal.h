@@ -130,10 +130,11 @@ struct MzhSearchPlan {
   int ohl;     // cooperative: the dynamics one-hot columns in LDS
   int sup33;   // 33-bin value / reward support (cooperative replay: always 1, one instantiation)
   int mmin;    // cooperative: caller-given MinMaxStats bounds (subnormal max - min check)
+  int occ2;    // cooperative: mzh_search_occ2_kernel<sup33, mmin> (16-root tile, two workgroups per CU)
 };
 
 size_t mzh_wave_smem_bytes(int S, int nt);
 hipError_t mzh_launch_wave_search(const MzhSearchPlan& pl, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream);
-size_t mzh_search_smem_bytes(int R, int S, bool ohl);
+size_t mzh_search_smem_bytes(int R, int S, bool ohl, bool occ2 = false);
 hipError_t mzh_launch_search(const MzhSearchPlan& pl, const MzhNet& net, const MzhSearchParams& p, hipStream_t stream);
 hipError_t mzh_launch_infer(int R, bool recurrent, const MzhNet& net, const MzhInferParams& p, hipStream_t stream);

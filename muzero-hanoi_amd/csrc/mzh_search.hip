@@ -32,11 +32,19 @@ constexpr int search_dc() { return R == 32 ? 16 : 32; }  // LDS-cached path dept
 
 // MMIN: the launch has caller-given MinMaxStats bounds (p.minmax_in), which could make max - min
 // subnormal: the selection then checks for that (MzhTree::select)
-template <int R, bool REPLAY, bool OHL, bool SUP33, bool MMIN>
-__global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, MzhSearchParams p) {
-  constexpr int DC = search_dc<R>();
+// C8: the two-workgroups-per-CU form (mzh_search_occ2_kernel): 16-root tile, <= 256 registers, the MLP
+// on 8-fragment weight chunks (mzh_mlp_recurrent_c8), DC = 16 cached path depths, no one-hot in LDS
+template <int R, int DC, bool C8, bool REPLAY, bool OHL, bool SUP33, bool MMIN>
+__device__ __forceinline__ void mzh_search_body(const MzhNet& net, const MzhSearchParams& p) {
+  static_assert(!C8 || (R == 16 && !OHL), "the 8-fragment MLP is the 16-root tile's");
+  constexpr int NF = C8 ? 8 : 16;  // fragments per weight buffer
   using Smem = SearchSmem<R, DC>;
-  constexpr int RPW = R / 4;  // roots per wave in the tree phases
+  // tree-phase waves: all four (R / 4 roots each), or for C8 two full waves of 8 roots -- waves 0-1 of one
+  // workgroup of a CU's pair, waves 2-3 of the other (workgroups b and b + 256 share a CU when 512 of them
+  // fill 256 CUs two deep), so each SIMD runs one 8-root tree wave per simulation as in the 32-root tile
+  // instead of two half-empty ones (the pairing is a placement guess: correctness does not depend on it)
+  constexpr int TRW = C8 ? 2 : 4;
+  constexpr int RPW = R / TRW;  // roots per tree wave
   constexpr int N2 = SUP33 ? 2 : 1;  // rwd2 / val2 MFMA tiles (bin 32 of a 33-bin head: vector chains)
   extern __shared__ __align__(16) unsigned char smem_raw[];
   MlpSmem<R>& sm = *reinterpret_cast<MlpSmem<R>*>(smem_raw);
@@ -55,8 +63,9 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
   const double disc = p.discount;
   const bool noised = p.noise != nullptr;
   // this lane's root (tree phases) and child slot
-  const int tr = wave * RPW + (lane >> 3), tc = lane & 7;
-  const bool tgroup = (lane >> 3) < RPW;  // wave-uniform per 8-lane group
+  const int tw = C8 ? wave - ((blockIdx.x >> 8) & 1) * 2 : wave;  // tree-wave index (wave-uniform)
+  const int tr = tw * RPW + (lane >> 3), tc = lane & 7;
+  const bool tgroup = (unsigned)tw < (unsigned)TRW && (lane >> 3) < RPW;  // wave-uniform per 8-lane group
 
   if (OHL)
     for (int i = tid; i < MZH_A * MZH_F; i += MZH_THREADS) ohl[i] = net.dyn0_onehot[i];
@@ -117,9 +126,14 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
     rb.P64[c] = v;
   }
   if (tid < R && tid >= nvalid) sm.act[tid] = 0;  // rows beyond the batch: any valid one-hot index
-  floatx4 fa[16], fb[16];
+  floatx4 fa[NF], fb[NF];
   float ba[4], bb[4];
-  if (!REPLAY) mzh_mlp_fetch12<R>(sm, net, wave, lane, fa, ba, fb, bb);
+  if (!REPLAY) {
+    if constexpr (C8)
+      mzh_mlp_fetch12_c8(sm, net, wave, lane, fa, ba, fb, bb);
+    else
+      mzh_mlp_fetch12<R>(sm, net, wave, lane, fa, ba, fb, bb);
+  }
   __syncthreads();
 
   MzhTree<R, DC, REPLAY, MlpSmem<R>> tree{p, st, sm, path, table, inv, root0, PL, lane, disc, noised};
@@ -142,7 +156,13 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
     // ---------------- expand via the network (mcts.py:88-106) ----------------
     if (!REPLAY) {
       MZH_STAMP(19);
-      mzh_mlp_recurrent_body<R, true, N2, false>(sm, net, wave, lane, fa, ba, fb, bb, OHL ? ohl : net.dyn0_onehot);
+      if constexpr (C8) {
+        // the previous simulation's last chunks loaded this one's A1 / A2 into the swapped buffers
+        if (s > 0) mzh_c8_swap(fa, ba, fb, bb);
+        mzh_mlp_recurrent_c8<N2>(sm, net, wave, lane, fa, ba, fb, bb, net.dyn0_onehot);
+      } else {
+        mzh_mlp_recurrent_body<R, true, N2, false>(sm, net, wave, lane, fa, ba, fb, bb, OHL ? ohl : net.dyn0_onehot);
+      }
       MZH_STAMP(20);
     }
     if (town) {
@@ -177,6 +197,18 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, 
     const int r = tid >> 3, c = tid & 7;
     if (r < nvalid && c == 0) tree.results(r);
   }
+}
+
+template <int R, bool REPLAY, bool OHL, bool SUP33, bool MMIN>
+__global__ __launch_bounds__(MZH_THREADS, 1) void mzh_search_kernel(MzhNet net, MzhSearchParams p) {
+  mzh_search_body<R, search_dc<R>(), false, REPLAY, OHL, SUP33, MMIN>(net, p);
+}
+
+// Two 16-root workgroups per CU (<= 256 registers, <= 80 KB LDS each): while one runs its MLP's MFMA
+// chains the other's tree phase (dependent block loads, fp64 chains) fills the SIMDs' stalls
+template <bool SUP33, bool MMIN>
+__global__ __launch_bounds__(MZH_THREADS, 2) void mzh_search_occ2_kernel(MzhNet net, MzhSearchParams p) {
+  mzh_search_body<16, 16, true, false, false, SUP33, MMIN>(net, p);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -218,9 +250,9 @@ __global__ __launch_bounds__(MZH_THREADS, 1) void mzh_recurrent_kernel(MzhNet ne
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
-template <int R>
+template <int R, int DC = search_dc<R>()>
 static size_t search_smem_bytes(int S, bool ohl) {
-  size_t b = sizeof(MlpSmem<R>) + sizeof(SearchSmem<R, search_dc<R>()>);
+  size_t b = sizeof(MlpSmem<R>) + sizeof(SearchSmem<R, DC>);
   b += sizeof(double) * 2 * (size_t)(S + 3);
   b += sizeof(uint16_t) * (size_t)((R * (S + 1) + 7) & ~7);
   if (ohl) b += sizeof(float) * MZH_A * MZH_F;
@@ -251,13 +283,30 @@ static hipError_t launch_search_t(const MzhSearchPlan& pl, const MzhNet& net, co
   return launch_search_s<R, REPLAY, OHL, false>(pl, net, p, stream);
 }
 
-// the LDS a search launch needs at tile R (ohl: with the dynamics one-hot columns in LDS)
-size_t mzh_search_smem_bytes(int R, int S, bool ohl) {
+// the LDS a search launch needs at tile R (ohl: with the dynamics one-hot columns in LDS; occ2: the
+// two-workgroups-per-CU kernel, 16 cached path depths)
+size_t mzh_search_smem_bytes(int R, int S, bool ohl, bool occ2) {
+  if (occ2) return search_smem_bytes<16, 16>(S, false);
   return R == 32 ? search_smem_bytes<32>(S, ohl) : search_smem_bytes<16>(S, ohl);
+}
+
+template <bool SUP33, bool MMIN>
+static hipError_t launch_search_occ2(const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
+  const size_t smem = search_smem_bytes<16, 16>(p.S, false);
+  const void* fn = reinterpret_cast<const void*>(&mzh_search_occ2_kernel<SUP33, MMIN>);
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  if (e != hipSuccess) return e;
+  const int grid = (p.B + 15) / 16;
+  hipLaunchKernelGGL((mzh_search_occ2_kernel<SUP33, MMIN>), dim3(grid), dim3(MZH_THREADS), smem, stream, net, p);
+  return hipGetLastError();
 }
 
 // the instantiation the plan names (mzh_api.hip make_plan decides every template argument)
 hipError_t mzh_launch_search(const MzhSearchPlan& pl, const MzhNet& net, const MzhSearchParams& p, hipStream_t stream) {
+  if (pl.occ2) {
+    if (pl.sup33) return pl.mmin ? launch_search_occ2<true, true>(net, p, stream) : launch_search_occ2<true, false>(net, p, stream);
+    return pl.mmin ? launch_search_occ2<false, true>(net, p, stream) : launch_search_occ2<false, false>(net, p, stream);
+  }
   if (pl.R == 32) {
     if (pl.replay) return launch_search_t<32, true, false>(pl, net, p, stream);
     if (pl.ohl) return launch_search_t<32, false, true>(pl, net, p, stream);

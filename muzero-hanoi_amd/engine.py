@@ -198,10 +198,12 @@ class Engine:
 
 
 def search_flags(kernel=None, tile=None, np1_ucb=False):
-    """mzh_search_args.flags for a kernel choice (None | "coop" | "wave" | "wave16") and coop tile"""
+    """mzh_search_args.flags for a kernel choice (None | "coop" | "occ2" | "wave" | "wave16") and coop tile
+    ("occ2": the cooperative kernel's two-workgroups-per-CU 16-root form)"""
     f = _lib.MZH_FLAG_NP1_UCB if np1_ucb else 0
     f |= {None: 0, "auto": 0, "coop": _lib.MZH_FLAG_KERNEL_COOP, "wave": _lib.MZH_FLAG_KERNEL_WAVE,
-          "wave16": _lib.MZH_FLAG_KERNEL_WAVE16}[kernel]
+          "wave16": _lib.MZH_FLAG_KERNEL_WAVE16,
+          "occ2": _lib.MZH_FLAG_KERNEL_COOP | _lib.MZH_FLAG_COOP_OCC2}[kernel]
     return f | {None: 0, 16: _lib.MZH_FLAG_COOP_TILE16, 32: _lib.MZH_FLAG_COOP_TILE32}[tile]
 
 

@@ -32,6 +32,7 @@ CONFIGS = {
     "c1_4096": (4, 4096, 50, 1, 0),          # configs[1]
     "c3_16384": (4, 16384, 200, 1, 0),       # configs[3]
     "c2_65536": (4, 65536, 50, 1, 0),        # configs[2], the metric's batch on one GPU
+    "c2_shard7of8": (4, 65536, 50, 8, 7),    # configs[2], rank 7's 8,192-root shard at N=8 (the 8-GPU headline)
     "c4_shard0of8": (7, 262144, 100, 8, 0),  # configs[4], rank 0's 32,768-root shard at N=8
 }
 SEED = 0

@@ -22,7 +22,7 @@ def gf():
     return gen_fullbatch
 
 
-@pytest.mark.parametrize("tag", ["c1_4096", "c3_16384", "c2_65536", "c4_shard0of8"])
+@pytest.mark.parametrize("tag", ["c1_4096", "c3_16384", "c2_65536", "c4_shard0of8", "c2_shard7of8"])
 def test_full_batch_fixture(gf, oracle, tag):
     z = golden(f"full_{tag}.npz")
     n, S = int(z["n_disks"]), int(z["n_sims"])

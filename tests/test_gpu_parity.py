@@ -181,9 +181,11 @@ def test_softmax_fallback_confident_heads_vs_oracle(mzh, oracle):
 
 # ------------------------------------------------------------------------------------ search
 KERNELS = ["coop", "wave", "wave16"]
+# MLP searches: also the two-workgroups-per-CU cooperative form (replay searches have no such form)
+KERNELS_MLP = KERNELS + ["occ2"]
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("kernel", KERNELS_MLP)
 def test_search_confident_heads_vs_oracle(mzh, oracle, kernel):
     """the fused searches with confident heads (softmax IEEE fallback inside the search kernels'
     heads) == the oracle's, every output bit for bit"""
@@ -229,7 +231,7 @@ def test_normalisation_exact_rerun_vs_oracle(mzh, oracle):
         assert np.array_equal(ri[k].cpu().numpy(), orr[k]), k
 
 
-@pytest.mark.parametrize("kernel,tile", [("coop", 16), ("coop", 32), ("wave", None), ("wave16", None)])
+@pytest.mark.parametrize("kernel,tile", [("coop", 16), ("coop", 32), ("wave", None), ("wave16", None), ("occ2", None)])
 def test_search_normalisation_exact_rerun_vs_oracle(mzh, oracle, kernel, tile):
     """the fused searches with every expansion's latent normalised by the exact-division rerun ==
     the oracle's, every output bit for bit (both cooperative tiles and the wave kernels)"""
@@ -290,7 +292,7 @@ def test_search_replay_bit_exact_vs_reference(mzh, case, kernel):
         assert list(out["latent"][b][:L]) == [int(v) for v in want[want >= 0]]
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("kernel", KERNELS_MLP)
 @pytest.mark.parametrize("case", [c for c in REPLAY_CASES if "shared" not in c])
 def test_search_mlp_end_to_end_vs_oracle(mzh, oracle, case, kernel):
     """Full fused search (MLP on MFMA) == oracle search with the same weights, bit for bit."""
@@ -317,7 +319,8 @@ def test_search_mlp_end_to_end_vs_oracle(mzh, oracle, case, kernel):
     assert agree.all(), f"{int(agree.sum())} / {len(agree)} histograms equal the reference's"
 
 
-@pytest.mark.parametrize("kernel,tile", [("coop", None), ("coop", 16), ("coop", 32), ("wave", None), ("wave16", None)])
+@pytest.mark.parametrize("kernel,tile", [("coop", None), ("coop", 16), ("coop", 32), ("wave", None), ("wave16", None),
+                                         ("occ2", None)])
 @pytest.mark.parametrize("B,S,n", [(40, 50, 4), (700, 25, 3), (9000, 8, 4), (300, 20, 7)])
 def test_search_batched_vs_oracle_random_roots(mzh, oracle, B, S, n, kernel, tile):
     """Ragged batches (not multiples of the 16/32-root tile), both tile sizes forced and by
@@ -364,11 +367,11 @@ def test_search_wave_equals_coop_large_batch(mzh, oracle, B, S, n, td):
     eng = _engine(mzh, n, S, B, sup, flat)
     tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
     res = {}
-    for kernel in KERNELS:
+    for kernel in KERNELS_MLP:
         o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0,
                        kernel=kernel)
         res[kernel] = {k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")}
-    for kernel in KERNELS[1:]:
+    for kernel in KERNELS_MLP[1:]:
         for k in res["coop"]:
             assert np.array_equal(res["coop"][k], res[kernel][k], equal_nan=True), (kernel, k)
     idx = np.r_[0:32, B - 40:B]
@@ -511,7 +514,8 @@ def test_search_caller_bounds_instantiation(mzh, oracle, B, tile):
 
 
 # ------------------------------------------------- whole-batch oracle parity at BASELINE sizes
-FULL_BATCH = ["c1_4096", "c3_16384", "c2_65536", "c4_shard0of8"]
+FULL_BATCH = [("c1_4096", None), ("c3_16384", None), ("c2_65536", None), ("c4_shard0of8", None),
+              ("c2_shard7of8", None), ("c2_shard7of8", "occ2"), ("c2_shard7of8", "coop"), ("c1_4096", "occ2")]
 
 
 def _first_diff(a, b):
@@ -519,8 +523,8 @@ def _first_diff(a, b):
     return None if bad.size == 0 else (int(bad[0]), int(bad.size))
 
 
-@pytest.mark.parametrize("tag", FULL_BATCH)
-def test_search_full_batch_equals_oracle(mzh, tag):
+@pytest.mark.parametrize("tag,kernel", FULL_BATCH)
+def test_search_full_batch_equals_oracle(mzh, tag, kernel):
     """EVERY root of each BASELINE.json search config at its full per-GPU size (configs[1] 4,096
     roots; configs[3] 16,384 x 200 sims; configs[2] 65,536 roots on one GPU; configs[4]'s rank-0
     shard at N=8, 32,768 7-disk roots x 100 sims), on bench.py's own inputs and reference-order
@@ -541,8 +545,10 @@ def test_search_full_batch_equals_oracle(mzh, tag):
     eng = _engine(mzh, n, S, B, sup, flat)
     tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
     o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0,
-                   deterministic=False, discount=0.8, eps=0.25)
+                   deterministic=False, discount=0.8, eps=0.25, kernel=kernel)
     kern = o["_plan"]["kernel"]
+    if kernel == "occ2":
+        assert kern.startswith("mzh_search_occ2_kernel<"), kern
     o = {k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")}
     eng.close()
     for k, want in (("visits", z["visits"]), ("action", z["action"]), ("sel_steps", z["sel_steps"]),
