@@ -26,12 +26,28 @@ __device__ __forceinline__ float dpp_max8(float v) {
   return v;
 }
 
-template <int MODE, int MPL, int VPL>
+// one 32-cycle unit of matrix work: one v_mfma_f32_16x16x4_f32 (K4 = 0), or four v_mfma_f32_4x4x1_16b_f32
+// (K4 = 1: the same 1,024 MACs and pipe time in 8-cycle instructions, so a co-resident wave's VALU waits
+// at most one short MFMA instead of a 32-cycle one)
+template <int K4>
+__device__ __forceinline__ floatx4 mf(float a, float b, floatx4 c) {
+  if (K4) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c = __builtin_amdgcn_mfma_f32_4x4x1f32(a, b + (float)i, c, 0, 0, 0);
+    return c;
+  }
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <int MODE, int MPL, int VPL, int K4 = 0>
 __global__ __launch_bounds__(512, 1) void k(const uint4* chase, float* out, unsigned long long* ticks, int levels) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint4* reg = chase + (size_t)blockIdx.x * NBLK * 8;
-  const bool do_mfma = MODE == 0 || MODE == 2 || MODE == 4 || (MODE == 3 && wave < 4);
-  const bool do_tree = MODE == 1 || MODE == 2 || MODE == 4 || (MODE == 3 && wave >= 4);
+  // modes 5 / 6: mode 3 with the tree waves / the MFMA waves at s_setprio 3 (the other at 0)
+  const bool pair = MODE == 3 || MODE == 5 || MODE == 6;
+  const bool do_mfma = MODE == 0 || MODE == 2 || MODE == 4 || (pair && wave < 4);
+  const bool do_tree = MODE == 1 || MODE == 2 || MODE == 4 || (pair && wave >= 4);
+  if ((MODE == 5 && wave >= 4) || (MODE == 6 && wave < 4)) __builtin_amdgcn_s_setprio(3);
   floatx4 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -49,14 +65,14 @@ __global__ __launch_bounds__(512, 1) void k(const uint4* chase, float* out, unsi
     if (do_tree && do_mfma) {
       const uint4 v = reg[(idx % NBLK) * 8 + (lane & 7)];
 #pragma unroll
-      for (int q = 0; q < MPL / 2; ++q) acc[q & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q & 7], b[q & 7], acc[q & 3], 0, 0, 0);
+      for (int q = 0; q < MPL / 2; ++q) acc[q & 3] = mf<K4>(a[q & 7], b[q & 7], acc[q & 3]);
       x = x + (double)v.y * 1e-9;
 #pragma unroll
       for (int q = 0; q < VPL; ++q) x = __builtin_fma(x, c1, c2);
       const float m = dpp_max8((float)x + (float)(lane & 7));
       idx = v.x + (m > 1e30f ? 1u : 0u);
 #pragma unroll
-      for (int q = MPL / 2; q < MPL; ++q) acc[q & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q & 7], b[q & 7], acc[q & 3], 0, 0, 0);
+      for (int q = MPL / 2; q < MPL; ++q) acc[q & 3] = mf<K4>(a[q & 7], b[q & 7], acc[q & 3]);
       if (MODE == 2) {
         // the load, MPL/2 MFMAs under it, then the chain interleaved 1 MFMA : 1 VALU
         __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // the load's address
@@ -77,7 +93,7 @@ __global__ __launch_bounds__(512, 1) void k(const uint4* chase, float* out, unsi
       idx = v.x + (m > 1e30f ? 1u : 0u);
     } else if (do_mfma) {
 #pragma unroll
-      for (int q = 0; q < MPL; ++q) acc[q & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q & 7], b[q & 7], acc[q & 3], 0, 0, 0);
+      for (int q = 0; q < MPL; ++q) acc[q & 3] = mf<K4>(a[q & 7], b[q & 7], acc[q & 3]);
     }
   }
   unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -102,10 +118,10 @@ __global__ __launch_bounds__(256, 1) void chase_lat(const uint4* chase, float* o
   if (lane == 0) ticks[blockIdx.x * 8 + wave] = t1 - t0;
 }
 
-template <int MODE, int MPL, int VPL>
+template <int MODE, int MPL, int VPL, int K4 = 0>
 static double run(const uint4* chase, float* out, unsigned long long* ticks, int levels) {
-  const int threads = MODE == 3 ? 512 : 256;
-  for (int rep = 0; rep < 2; ++rep) hipLaunchKernelGGL((k<MODE, MPL, VPL>), dim3(256), dim3(threads), 0, 0, chase, out, ticks, levels);
+  const int threads = (MODE == 3 || MODE == 5 || MODE == 6) ? 512 : 256;
+  for (int rep = 0; rep < 2; ++rep) hipLaunchKernelGGL((k<MODE, MPL, VPL, K4>), dim3(256), dim3(threads), 0, 0, chase, out, ticks, levels);
   hipDeviceSynchronize();
   std::vector<unsigned long long> h(256 * 8);
   hipMemcpy(h.data(), ticks, h.size() * 8, hipMemcpyDeviceToHost);
@@ -148,6 +164,20 @@ static std::vector<uint32_t> make_chase(int nblk) {
       for (int w = 0; w < 32; ++w) host[((size_t)b * nblk + perm[i]) * 32 + w] = (w % 4 == 0) ? perm[(i + 1) % nblk] : 1000u + w;
   }
   return host;
+}
+
+// the same two-waves-per-SIMD pairing with the matrix work as 8-cycle 4x4x1 MFMAs
+template <int MPL, int VPL>
+static void sweep_k4(const uint4* chase, float* out, unsigned long long* ticks) {
+  const int L = 2000;
+  const double m0 = run<0, MPL, VPL, 1>(chase, out, ticks, L), m1 = run<1, MPL, VPL, 1>(chase, out, ticks, L);
+  const double m3 = run<3, MPL, VPL, 1>(chase, out, ticks, L);
+  const double m5 = run<5, MPL, VPL, 1>(chase, out, ticks, L), m6 = run<6, MPL, VPL, 1>(chase, out, ticks, L);
+  const double p5 = run<5, MPL, VPL, 0>(chase, out, ticks, L), p6 = run<6, MPL, VPL, 0>(chase, out, ticks, L);
+  printf("{\"mfma_4x4x1_units_per_level\": %d, \"fp64_chain_per_level\": %d, \"ticks_per_level\": {\"mfma_alone\": %.1f, "
+         "\"tree_alone\": %.1f, \"two_waves_per_simd\": %.1f, \"two_waves_tree_prio\": %.1f, \"two_waves_mfma_prio\": %.1f, "
+         "\"16x16x4_two_waves_tree_prio\": %.1f, \"16x16x4_two_waves_mfma_prio\": %.1f}, \"sum\": %.1f, \"max\": %.1f}\n",
+         MPL, VPL, m0, m1, m3, m5, m6, p5, p6, m0 + m1, m0 > m1 ? m0 : m1);
 }
 
 int main() {
@@ -194,5 +224,9 @@ int main() {
   sweep<48, 24>(chase, out, ticks);
   sweep<48, 48>(chase, out, ticks);
   sweep<96, 24>(chase, out, ticks);
+  sweep_k4<16, 8>(chase, out, ticks);
+  sweep_k4<32, 16>(chase, out, ticks);
+  sweep_k4<48, 24>(chase, out, ticks);
+  sweep_k4<96, 24>(chase, out, ticks);
   return 0;
 }
