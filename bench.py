@@ -55,10 +55,17 @@ SEL_BYTES, BACKUP_BYTES, EXPAND_BYTES = 124, 28, 540
 EXPAND_BYTES_REPLAY = 32 + 28
 
 # one dependent 128-B tree-block load (an 8-lane group's slot reads, L2-resident footprint, one wave per
-# SIMD on every CU) and the s_memtime rate: tools/micro/overlap_probe.hip, profiles/r04_overlap_probe.json
-TREE_LOAD_NS = 136.1          # 16 MB footprint (L2-resident): the floor's latency
-TREE_LOAD_NS_MALL = 331.5     # 128 MB footprint (Infinity-Cache-resident), reported beside it
-TREE_LOAD_FOOTPRINT = "dependent 128-B block loads, 16 MB footprint over 256 CUs (L2-resident), one wave per SIMD"
+# SIMD on every CU): tools/micro/overlap_probe.hip, profiles/r04_overlap_probe.json -- the strict floor
+TREE_LOAD_NS = 136.1
+# loaded latency of a random 128-B line at the search kernels' concurrency (tools/micro/tree_mem_probe.hip,
+# profiles/r05_tree_mem_probe.json: 2,048 waves, two per SIMD, each with W walks of dependent block loads,
+# a lane pair per walk, uniformly random over F bytes): ns per dependent level by (footprint MB, walks per wave)
+TREE_PROBE_NS = {(16, 1): 314.2, (16, 8): 368.4, (16, 32): 890.6,
+                 (128, 1): 315.8, (128, 8): 375.8, (128, 32): 1216.2,
+                 (448, 1): 316.6, (448, 8): 539.0, (448, 32): 1221.7,
+                 (1344, 1): 317.4, (1344, 8): 589.4, (1344, 32): 1206.7}
+# the same probe's random-line throughput with all 32 walks per wave streaming (no dependency), 448 MB footprint
+TREE_RANDOM_LINE_GBPS = 6757.3
 
 METRIC = "MCTS sims/sec (node) 4-disk Hanoi, 50 sims/move, 65k root batch; 1/2/4/8 GPU"
 # BASELINE.json configs[1..4]: (disks, global roots, sims, description)
@@ -326,29 +333,51 @@ def lookup_traffic(path, key):
     return ent, "rocprofv3 PMC of this build (tools/prof.sh + tools/traffic.py)"
 
 
-def tree_latency_floor(sel_steps, S, plan, load_ns=None):
-    """A latency ceiling for select/backup (beside the HBM one): per simulation every lockstep group --
-    the cooperative kernel's workgroup of R roots, the wave kernel's wave of 16 NT roots -- waits for
-    its deepest root's selection, whose levels below the root are dependent block loads (the root level
-    is in LDS).  With d_r = sel_steps_r / S - 1 (root r's mean dependent loads per simulation) the
-    group needs at least S * max_r d_r loads in sequence; groups run concurrently on the GPU's slots
-    (256 CUs x 1 cooperative workgroup; 2,048 wave slots: 2 waves per SIMD).  Floor = rounds x S x
-    mean over groups of max_r d_r x the measured dependent-load latency.  max of the per-root MEANS is
-    below the mean of the per-simulation maxima, so this is a lower bound on the tree kernel's time."""
-    load_ns = TREE_LOAD_NS if load_ns is None else load_ns
-    d = np.asarray(sel_steps, np.float64) / S - 1.0
+def probe_latency_ns(footprint_mb, walks_per_wave):
+    """TREE_PROBE_NS interpolated: log-linear in the footprint, linear in the walks per wave (clamped)"""
+    fps = sorted({f for f, _ in TREE_PROBE_NS})
+    ws = sorted({w for _, w in TREE_PROBE_NS})
+    f = min(max(footprint_mb, fps[0]), fps[-1])
+    w = min(max(walks_per_wave, ws[0]), ws[-1])
+
+    def lerp(xs, x, fn, log=False):
+        for a, b in zip(xs, xs[1:]):
+            if a <= x <= b:
+                t = (np.log(x) - np.log(a)) / (np.log(b) - np.log(a)) if log else (x - a) / (b - a)
+                return fn(a) * (1 - t) + fn(b) * t
+        return fn(xs[-1])
+
+    return lerp(fps, f, lambda ff: lerp(ws, w, lambda ww: TREE_PROBE_NS[(ff, ww)]), log=True)
+
+
+def tree_latency_model(levels, S, plan, B, kernel_ms=None):
+    """The select / backup latency ceiling from the kernel's own count: every lockstep group (a wave of
+    the wave kernel, a workgroup of the cooperative kernels) waits, simulation after simulation, for its
+    deepest root's dependent tree-block loads -- `levels[g]` of them in all (mzh_search_args.lockstep_levels).
+    The groups of one round run concurrently, so the launch takes at least max_g levels[g] x the latency
+    of one such load.  Priced twice: `floor_ms` with the L2-resident latency (a strict lower bound) and
+    `model_ms` with the probe's loaded latency of a random 128-B line at this launch's footprint and
+    walks per wave (TREE_PROBE_NS) -- the latency the levels actually see when every group walks at once."""
+    lv = np.asarray(levels, np.float64)
     g = plan["roots_per_wave"] if plan["wave"] else plan["roots_per_workgroup"]
-    n = -(-len(d) // g)
-    dd = np.zeros(n * g)
-    dd[: len(d)] = d
-    gmax = dd.reshape(n, g).max(1)
+    n = -(-B // g)
+    lv = lv[:n]
     slots = lockstep_slots(plan)
     rounds = -(-n // slots)
-    floor_ms = rounds * S * float(gmax.mean()) * load_ns * 1e-6
-    return {"floor_ms": floor_ms, "floor_ms_mall": floor_ms * TREE_LOAD_NS_MALL / load_ns,
-            "groups": n, "roots_per_group": g, "rounds": rounds,
-            "mean_group_max_loads_per_sim": float(gmax.mean()), "mean_loads_per_sim": float(d.mean()),
-            "load_ns": load_ns, "load_footprint": TREE_LOAD_FOOTPRINT}
+    deepest = float(lv.max()) if rounds == 1 else float(rounds * lv.mean())
+    walks = plan["roots_per_wave"]  # walks in flight per wave: its roots (cooperative: R / 4 per wave)
+    footprint_mb = B * (S + 1) * 128 / 2 ** 20
+    lat = probe_latency_ns(footprint_mb, walks)
+    out = {"groups": n, "roots_per_group": g, "rounds": rounds,
+           "levels_per_sim": {"mean_group": float(lv.mean()) / S, "max_group": float(lv.max()) / S},
+           "floor_ms": deepest * TREE_LOAD_NS * 1e-6, "floor_load_ns": TREE_LOAD_NS,
+           "model_ms": deepest * lat * 1e-6, "model_load_ns": lat,
+           "model_probe": {"footprint_mb": footprint_mb, "walks_per_wave": walks,
+                           "source": "tools/micro/tree_mem_probe.hip, profiles/r05_tree_mem_probe.json"}}
+    if kernel_ms:
+        out["floor_frac"] = out["floor_ms"] / kernel_ms
+        out["frac"] = out["model_ms"] / kernel_ms
+    return out
 
 
 CUS = 256                  # MI355X: 8 XCDs x 32 CUs
@@ -558,8 +587,15 @@ def main():
             eng.search(S, replay=rp, tie_idx=tie, noise=noise, action_u=u, temperature=1.0, deterministic=False,
                        discount=0.8, eps=0.25, out=rout, kernel=kern, tile=a.tile)
 
+        # one untimed launch also counts each lockstep group's selection levels (the latency model's input;
+        # the timed launches below do not count, so the count costs them nothing)
+        lout = eng.alloc_search_outputs(B, S, lockstep=True)
+        eng.search(S, replay=rp, tie_idx=tie, noise=noise, action_u=u, temperature=1.0, deterministic=False,
+                   discount=0.8, eps=0.25, out=lout, kernel=kern, tile=a.tile)
         replay()
         torch.cuda.synchronize(dev)
+        assert torch.equal(lout["visits"], rout["visits"]), "the level count changed the search"
+        levels = lout["lockstep_levels"].cpu().numpy()
         rsel = float(rout["sel_steps"].double().sum())
         tev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
         for s_, e_ in tev:
@@ -574,18 +610,23 @@ def main():
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s", "sel_steps_per_sim": rsel / (B * S),
                 "frac": tb / (tree_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "traffic": None,
                 "fused_tree_bytes_per_launch": tree_bytes(sel_sum, B, S, EXPAND_BYTES),
-                "latency": tree_latency_floor(rout["sel_steps"].cpu().numpy(), S, rout["_plan"]),
+                "random_line": {"ceiling_gbps": TREE_RANDOM_LINE_GBPS,
+                                "frac": tb / (tree_ms * 1e-3) / 1e9 / TREE_RANDOM_LINE_GBPS,
+                                "what": "the same bytes against the random 128-B line throughput the probe measured "
+                                        "at this concurrency (tools/micro/tree_mem_probe.hip), not the streaming peak"},
+                "latency": tree_latency_model(levels, S, rout["_plan"], B, tree_ms),
                 "what": "select/expand/backup only: the search kernel's replay instantiation (same tree code, "
                         "network outputs read from HBM), same roots and draws; bytes = SURVEY.md 8d (124 B per "
                         "selection step, 28 B per backed-up node, 60 B per replayed expansion) with the kernel's "
                         "own selection-step count; fused_tree_bytes_per_launch: the same count in the fused "
                         "search (540 B per expansion incl. the latent read/write)"}
 
-    if tree is not None and tree["latency"] is not None:
-        tree["latency"]["frac"] = tree["latency"]["floor_ms"] / tree["kernel_ms"]
-        tree["latency"]["what"] = ("fraction of the tree kernel's HIP-event time that its deepest roots' dependent "
-                                   "block loads alone take (bench.tree_latency_floor); the HBM frac beside it "
-                                   "prices bytes, this one the load-latency chain")
+    if tree is not None:
+        tree["latency"]["what"] = ("fraction of the tree kernel's HIP-event time that its lockstep groups' dependent "
+                                   "block loads take in sequence (kernel-counted levels x the probe's loaded "
+                                   "latency; floor_frac with the L2-resident latency), bench.tree_latency_model")
+        fr = {"hbm": tree["frac"], "random_line": tree["random_line"]["frac"], "latency": tree["latency"]["frac"]}
+        tree["binding"] = {"ceiling": max(fr, key=fr.get), "frac": max(fr.values()), "fracs": fr}
     dinfo = None
     if dist is not None:
         # every rank's own figures, gathered (so a scaling record shows the ranks RCCL saw), then maxed
@@ -610,6 +651,11 @@ def main():
             tree["kernel_ms"] = float(t[2])
             tree["achieved"] = tree["bytes_per_launch"] / (tree["kernel_ms"] * 1e-3) / 1e9
             tree["frac"] = tree["achieved"] / HBM_PEAK_GBPS
+            tree["random_line"]["frac"] = tree["achieved"] / TREE_RANDOM_LINE_GBPS
+            tree["latency"]["frac"] = tree["latency"]["model_ms"] / tree["kernel_ms"]
+            tree["latency"]["floor_frac"] = tree["latency"]["floor_ms"] / tree["kernel_ms"]
+            fr = {"hbm": tree["frac"], "random_line": tree["random_line"]["frac"], "latency": tree["latency"]["frac"]}
+            tree["binding"] = {"ceiling": max(fr, key=fr.get), "frac": max(fr.values()), "fracs": fr}
 
     sims_total = (GB if a.shard is None else B) * S * a.steps
     value = sims_total / dt

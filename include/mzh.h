@@ -167,6 +167,12 @@ typedef struct mzh_search_args {
    * exponent (integer exponents are exact products); without it the device pow is used, which can
    * differ from NumPy's vectorised pow in the last bit. */
   const double* pow_table;
+  /* [lockstep groups] (nullable; entries of groups without roots are left untouched): per group of roots
+   * that advance through a simulation together -- a wave of the wave kernel (16 or 32 roots, index
+   * blockIdx * 4 + wave), a workgroup of the cooperative kernels -- the sum over simulations of the
+   * group's deepest selection below the root, i.e. the dependent tree-block loads the group waits for in
+   * sequence (the select / backup latency model, bench.py roofline.tree.latency) */
+  int32_t* lockstep_levels;
   /* HOST pointer (nullable): filled with the plan of the launched instantiation (below); B = 0
    * launches nothing and reports kernel "none" */
   struct mzh_search_plan* plan_out;

@@ -51,7 +51,7 @@ class SearchArgs(ctypes.Structure):
         ("obs", _vp), ("noise", _vp), ("tie_idx", _vp), ("action_u", _vp), ("minmax_in", _vp),
         ("rp_root_pi", _vp), ("rp_sim", _vp),
         ("visits", _vp), ("root_q", _vp), ("minmax_out", _vp), ("extra_ties", _vp), ("action", _vp),
-        ("pi", _vp), ("latent", _vp), ("latent_len", _vp), ("sel_steps", _vp), ("pow_table", _vp),
+        ("pi", _vp), ("latent", _vp), ("latent_len", _vp), ("sel_steps", _vp), ("pow_table", _vp), ("lockstep_levels", _vp),
         ("plan_out", ctypes.POINTER(SearchPlan)),
     ]
 

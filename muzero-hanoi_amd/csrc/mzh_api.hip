@@ -596,7 +596,7 @@ static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream s
   p.rp_root_pi = a->rp_root_pi; p.rp_sim = a->rp_sim;
   p.tree = eng->tree; p.htree = eng->htree; p.pathx = eng->pathx; p.table = eng->table;
   p.visits = a->visits; p.root_q = a->root_q; p.minmax_out = a->minmax_out; p.extra_ties = a->extra_ties;
-  p.action = a->action; p.pi = a->pi; p.latent = a->latent; p.latent_len = a->latent_len; p.sel_steps = a->sel_steps;
+  p.action = a->action; p.pi = a->pi; p.latent = a->latent; p.latent_len = a->latent_len; p.sel_steps = a->sel_steps; p.lockstep_levels = a->lockstep_levels;
   p.pow_table = a->pow_table;
   hipError_t e = pl.wave ? mzh_launch_wave_search(pl, eng->wnet, p, (hipStream_t)stream)
                          : mzh_launch_search(pl, eng->net, p, (hipStream_t)stream);

@@ -32,6 +32,7 @@ struct MzhSearchParams {
   int32_t* latent_len;
   int32_t* sel_steps;
   const double* pow_table;  // [S + 1] np.power(n, 1/T) for a non-integer exponent (nullable)
+  int32_t* lockstep_levels;  // [groups] sum over simulations of each lockstep group's deepest selection (nullable)
 };
 
 // visits ** e as generate_play_policy computes it (np.power(int64 visits, e), mcts.py:168-174), for

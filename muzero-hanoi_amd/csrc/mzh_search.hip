@@ -149,9 +149,27 @@ __device__ __forceinline__ void mzh_search_body(const MzhNet& net, const MzhSear
   const bool town = tgroup && tr < nvalid;
   if (town) rs.load(st, tr);
 
+  // p.lockstep_levels: the workgroup's deepest selection below the root per simulation (every wave's
+  // maximum through LDS, read by thread 0 after the simulation's closing barrier)
+  const bool lcount = p.lockstep_levels != nullptr;
+  int lsum = 0;
+  auto wave_level = [&]() {
+    int m = town ? rs.depth - 1 : 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off));
+    if (lane == 0) st.lvl[wave] = m;
+  };
+  auto group_level = [&]() {
+    int m = st.lvl[0];
+#pragma unroll
+    for (int w = 1; w < MZH_WAVES; ++w) m = max(m, st.lvl[w]);
+    lsum += m;
+  };
   MZH_STAMP_DECL
   if (town) tree.template select<MMIN>(tr, tc, 0, rs);
+  if (lcount) wave_level();
   __syncthreads();
+  if (lcount && tid == 0 && S > 0) group_level();
   for (int s = 0; s < S; ++s) {
     // ---------------- expand via the network (mcts.py:88-106) ----------------
     if (!REPLAY) {
@@ -186,9 +204,12 @@ __device__ __forceinline__ void mzh_search_body(const MzhNet& net, const MzhSear
         MZH_STAMP(30);
       }
     }
+    if (lcount && s + 1 < S) wave_level();
     __syncthreads();
+    if (lcount && tid == 0 && s + 1 < S) group_level();
     MZH_STAMP(23);
   }
+  if (lcount && tid == 0) p.lockstep_levels[blockIdx.x] = lsum;
 
   // ---------------- results (mcts.py:111-126, 154-176) ----------------
   if (town && tc == 0) rs.store(st, tr);

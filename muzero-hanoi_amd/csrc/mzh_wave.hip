@@ -476,6 +476,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
   }
   double den = mmax - mmin, dinv = mmax > mmin ? 1.0 / (mmax - mmin) : 0.0;
   int firstTie = 0, extra = 0, steps = 0, rootN = 0, depth = 0, leafE = 0, leafA = 0;
+  int lsum = 0;  // p.lockstep_levels: the wave's deepest selection below the root, summed over simulations
   double rootW = 0.0;
   const int tie = (rvalid && p.tie_idx) ? p.tie_idx[rroot] : 0;
 
@@ -674,6 +675,12 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
       leafE = e;
       leafA = pick;
       steps += d;
+    }
+    if (p.lockstep_levels) {  // wave-uniform: only when the caller asks for the latency model's input
+      int m = rvalid ? depth - 1 : 0;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off));
+      lsum += m;
     }
     if (!REPLAY) {
 #pragma unroll
@@ -905,6 +912,7 @@ __global__ __launch_bounds__(MZW_WAVES * 64, 2) void mzh_wave_kernel(MzhWNet net
   }
 
   // ---------------- results (mcts.py:111-126, 154-176) ----------------
+  if (p.lockstep_levels && lane == 0) p.lockstep_levels[blockIdx.x * MZW_WAVES + wave] = lsum;
   if (!rvalid || half) return;
   const int root = rroot;
   int vis[MZH_A];

@@ -109,9 +109,12 @@ class Engine:
         return out
 
     # ---------------------------------------------------------------- search
-    def alloc_search_outputs(self, B, n_sims):
+    def alloc_search_outputs(self, B, n_sims, lockstep=False):
+        """lockstep=True adds lockstep_levels (zeroed, one entry per group of roots that advance together:
+        B // 16 + 1 covers every kernel's groups)"""
         d = self.device
-        return dict(
+        extra = {"lockstep_levels": torch.zeros(B // 16 + 1, dtype=torch.int32, device=d)} if lockstep else {}
+        return dict(**extra,
             visits=torch.empty((B, ACTIONS), dtype=torch.int32, device=d),
             root_q=torch.empty(B, dtype=torch.float64, device=d),
             minmax=torch.empty((B, 2), dtype=torch.float64, device=d),
@@ -188,6 +191,7 @@ class Engine:
         if pt is not None:
             keep.append(pt)
         a.pow_table = ptr(pt)
+        a.lockstep_levels = ptr(out.get("lockstep_levels"))
         plan = _lib.SearchPlan()
         a.plan_out = ctypes.pointer(plan)
         fn = _lib.lib().mzh_search_replay if replay is not None else _lib.lib().mzh_search

@@ -64,7 +64,7 @@ def test_search_args_layout_matches_header(lib, tmp_path):
     block = hdr[hdr.index("typedef struct mzh_search_args"):]
     block = block[:block.index("} mzh_search_args;")]
     n_ptr_fields = len(re.findall(r"^\s+(?:const\s+|struct\s+)?\w+\*\s+\w+;", block, re.M))
-    assert n_ptr_fields == 18 == len(fields) - 7
+    assert n_ptr_fields == 19 == len(fields) - 7
 
 
 def test_search_plan_layout_matches_header(lib, tmp_path):

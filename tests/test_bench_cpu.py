@@ -85,23 +85,30 @@ def test_physical_core_count():
     assert 1 <= n <= len(cpus)
 
 
-def test_tree_latency_floor():
-    """the select/backup latency ceiling: deepest root per lockstep group x dependent-load latency"""
+def test_tree_latency_model():
+    """the select/backup latency ceiling: each lockstep group's kernel-counted levels (its deepest root's
+    dependent block loads, summed over simulations) x the load latency; the probe latency interpolates
+    between the measured footprints and walks per wave"""
     import numpy as np
 
     import bench
 
     S = 50
     pl = bench.search_plan(S, 8192)  # cooperative: 32-root workgroups, 256 of them = one round
-    steps = np.full(8192, 3 * S)  # every root 3 levels per simulation = 2 dependent block loads
-    steps[::32] = 6 * S  # the deepest root of each group: 5 loads
-    f = bench.tree_latency_floor(steps, S, pl, load_ns=100.0)
+    levels = np.full(256, 3 * S)
+    levels[7] = 5 * S  # the slowest group: 5 levels per simulation
+    f = bench.tree_latency_model(levels, S, pl, 8192, kernel_ms=1.0)
     assert f["roots_per_group"] == 32 and f["groups"] == 256 and f["rounds"] == 1
-    assert abs(f["mean_group_max_loads_per_sim"] - 5.0) < 1e-12
-    assert abs(f["floor_ms"] - S * 5 * 100e-6) < 1e-12
+    assert abs(f["levels_per_sim"]["max_group"] - 5.0) < 1e-12
+    assert abs(f["floor_ms"] - 5 * S * bench.TREE_LOAD_NS * 1e-6) < 1e-12
+    assert abs(f["model_ms"] - 5 * S * f["model_load_ns"] * 1e-6) < 1e-12 and f["frac"] == f["model_ms"]
+    # 8 walks per wave (the 32-root tile's waves), 8,192 x 51 x 128 B = 51 MB: between the probe's points
+    assert bench.TREE_PROBE_NS[(16, 8)] < f["model_load_ns"] < bench.TREE_PROBE_NS[(128, 8)]
     pw = bench.search_plan(S, 262144)  # wave kernel: 32-root waves, 8,192 waves = 4 rounds of 2,048 slots
-    f = bench.tree_latency_floor(np.full(262144, 2 * S), S, pw, load_ns=100.0)
-    assert f["roots_per_group"] == 32 and f["rounds"] == 4 and abs(f["floor_ms"] - 4 * S * 1 * 100e-6) < 1e-12
+    f = bench.tree_latency_model(np.full(8192, 2 * S), S, pw, 262144)
+    assert f["roots_per_group"] == 32 and f["rounds"] == 4
+    assert abs(f["model_ms"] - 4 * 2 * S * bench.TREE_PROBE_NS[(1344, 32)] * 1e-6) < 1e-9
+    assert bench.probe_latency_ns(448, 32) == bench.TREE_PROBE_NS[(448, 32)]
 
 
 def test_traffic_summary_keeps_the_bench_instantiation(tmp_path):

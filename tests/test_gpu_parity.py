@@ -560,3 +560,33 @@ def test_search_full_batch_equals_oracle(mzh, tag, kernel):
     assert d is None, f"{tag} ({kern}): root Q / MinMaxStats differ in 256-root block {d[0]} ({d[1]} blocks)"
     if "root_q" in z:
         assert np.array_equal(o["root_q"], z["root_q"]) and np.array_equal(o["minmax"], z["minmax"])
+
+
+@pytest.mark.parametrize("kernel,tile", [("coop", 16), ("coop", 32), ("occ2", None), ("wave", None), ("wave16", None)])
+def test_search_lockstep_levels(mzh, oracle, kernel, tile):
+    """mzh_search_args.lockstep_levels (the select/backup latency model's input, bench.tree_latency_model):
+    per lockstep group the sum over simulations of its deepest selection below the root, so
+    max_r (sel_steps_r - S) <= levels_g <= sum_r (sel_steps_r - S) over the group's roots; asking for
+    it changes no other output (fused and replay searches)"""
+    from muzero_hanoi_amd import _lib
+
+    B, S, n = 2000, 30, 4
+    flat, in_dim, sup = _weights(oracle, f"weights_N{n}_s0")
+    obs, noise, tie, u = _random_search_inputs(B, n, 4321)
+    eng = _engine(mzh, n, S, B, sup, flat)
+    tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
+    kw = dict(obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0, kernel=kernel, tile=tile)
+    base = eng.search(S, **kw)
+    lo = eng.search(S, out=eng.alloc_search_outputs(B, S, lockstep=True), **kw)
+    pl = lo["_plan"]
+    for k in ("visits", "root_q", "pi", "action", "sel_steps", "minmax"):
+        assert torch.equal(base[k], lo[k]), k
+    g = pl["roots_per_wave"] if pl["wave"] else pl["roots_per_workgroup"]
+    ng = -(-B // g)
+    lv = lo["lockstep_levels"].cpu().numpy()
+    assert (lv[ng:] == 0).all()
+    below = lo["sel_steps"].cpu().numpy().astype(np.int64) - S  # each simulation's levels below the root
+    for grp in range(ng):
+        d = below[grp * g:(grp + 1) * g]
+        assert d.max() <= lv[grp] <= d.sum(), (grp, lv[grp], d.max(), d.sum())
+    assert pl == _lib.search_plan(sup, B, S, mzh.search_flags(kernel, tile))
