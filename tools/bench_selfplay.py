@@ -7,13 +7,15 @@ config: N=3, max_steps=200, S=25, T=1 stochastic, random-init MuZeroNet(TD_retur
 Legs:
   batched   B episodes in lockstep on one GPU (selfplay.BatchedSelfPlay: one search launch and one
             env-kernel launch per move over every unfinished episode)
+  batched-legacy  the same with every draw from NumPy's global legacy stream in the reference's
+            order (legacy_rng=True; rng.predraw, the bit-exact mode)
   drop-in   the reference's sequential loop through the drop-ins (selfplay.play_game: one
             MCTS.run_mcts launch and one env.step per decision, as Muzero._play_game runs it)
   cpu       the reference algorithm on one host core (bench.cpu_baseline_selfplay: oracle/py_port.py's
             object-tree MCTS with a batch-1 torch-CPU MLP + the C env restatement), bounded to
             --cpu-seconds
 
-  python tools/bench_selfplay.py [--legs batched,drop-in,cpu] [--episodes 4096] [--sims 25]
+  python tools/bench_selfplay.py [--legs batched,batched-legacy,drop-in,cpu] [--episodes 4096] [--sims 25]
 """
 import argparse
 import json
@@ -41,6 +43,25 @@ def leg_batched(args, net):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     res = sp.play(start_states(args.disks, args.episodes, 2), seed=2)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    moves = int(res["steps"].sum())
+    return dict(decisions=moves, episodes=args.episodes, seconds=dt,
+                solved=int((res["steps"] < args.max_steps).sum()))
+
+
+def leg_batched_legacy(args, net):
+    """the batched leg with every draw from NumPy's global legacy stream in the reference's order
+    (legacy_rng=True: rng.predraw per move over the unfinished episodes) -- the bit-exact mode"""
+    from muzero_hanoi_amd.selfplay import BatchedSelfPlay
+
+    sp = BatchedSelfPlay(net, args.disks, args.max_steps, args.sims)
+    np.random.seed(1)
+    sp.play(start_states(args.disks, min(args.episodes, 256), 1), legacy_rng=True)  # warm-up
+    torch.cuda.synchronize()
+    np.random.seed(2)
+    t0 = time.perf_counter()
+    res = sp.play(start_states(args.disks, args.episodes, 2), legacy_rng=True)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     moves = int(res["steps"].sum())
@@ -96,7 +117,8 @@ def main():
         dev = "cpu" if leg == "cpu" else "cuda"
         torch.manual_seed(1)
         net = MuZeroNet(3 * args.disks, 6, 0.002, dev, TD_return=True).to(dev)
-        r = {"batched": leg_batched, "drop-in": leg_dropin, "cpu": leg_cpu}[leg](args, net)
+        r = {"batched": leg_batched, "batched-legacy": leg_batched_legacy, "drop-in": leg_dropin,
+             "cpu": leg_cpu}[leg](args, net)
         r.update(leg=leg, metric="selfplay_decisions_per_sec", value=r["decisions"] / r["seconds"],
                  unit="decisions/s", sims_per_sec=r["decisions"] * args.sims / r["seconds"],
                  config={"workload": f"hanoi{args.disks}_s{args.sims}_maxsteps{args.max_steps}",
