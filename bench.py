@@ -670,6 +670,14 @@ def main():
     traffic = tent.get("hbm_bytes_per_launch") if tent else None
     if tree is not None and tent:
         tree["traffic"] = tent.get("tree_hbm_bytes_per_launch")
+        if tent.get("tree_issue_frac") is not None:
+            # the issue ceiling: the fraction of the SIMDs' cycles some wave issued (PMC of this build)
+            tree["issue"] = {"frac": tent["tree_issue_frac"], "waitcnt_frac": tent.get("tree_waitcnt_frac"),
+                             "source": "rocprofv3 --pmc SQ_ACTIVE_INST_ANY x 4 / (1,024 SIMDs x GRBM_GUI_ACTIVE / 8) "
+                                       "of this build (tools/prof.sh + tools/traffic.py)"}
+            tree["binding"]["fracs"]["issue"] = tent["tree_issue_frac"]
+            b = tree["binding"]["fracs"]
+            tree["binding"].update(ceiling=max(b, key=b.get), frac=max(b.values()))
 
     if weak:
         workload = (f"weak scaling: {N}-disk, {B} roots per GPU ({GB} over {world} GPUs), {S} sims/move "

@@ -76,6 +76,12 @@ def summarise(root, tag, want=None):
             cyc = d["GRBM_GUI_ACTIVE"] / 8
             d["clock_ghz"] = cyc / d["avg_ns"]
             d["mfma_busy_frac"] = d["SQ_INSTS_MFMA"] * 32 / (cyc * 1024)
+            if "SQ_ACTIVE_INST_ANY" in d:
+                # the issue ceiling: cycles some wave of a SIMD issued (SQ_ACTIVE_INST_ANY counts quad-cycles per
+                # wave, summed over waves) over the SIMDs' cycles
+                d["issue_frac"] = d["SQ_ACTIVE_INST_ANY"] * 4 / (cyc * 1024)
+        if "SQ_WAIT_ANY" in d and "SQ_WAVE_CYCLES" in d:
+            d["waitcnt_frac"] = d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"]  # wave cycles parked in s_waitcnt
     return out
 
 
@@ -157,6 +163,8 @@ def main():
             "tree_kernel": t.get("kernel"), "tree_avg_ns": t.get("avg_ns"),
             "tree_hbm_bytes_per_launch": t.get("hbm_bytes_per_launch"),
             "tree_read_bytes_corrected": t.get("hbm_read_bytes_corrected"), "tree_write_bytes": t.get("hbm_write_bytes"),
+            "tree_issue_frac": t.get("issue_frac"), "tree_waitcnt_frac": t.get("waitcnt_frac"),
+            "issue_frac": f.get("issue_frac"),
             "unprofiled_kernel_ms": (out.get("unprofiled") or {}).get("kernel_ms_hip_events"),
             "source": f"tools/prof.sh TAG={a.tag} + tools/traffic.py: rocprofv3 --kernel-trace --stats and separate "
                       "--pmc passes of the bench command; FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, "
