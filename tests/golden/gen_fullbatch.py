@@ -4,6 +4,9 @@ test_search_full_batch_equals_oracle) compares EVERY root of the HIP search with
 
     python tests/golden/gen_fullbatch.py [TAG ...]        # ~10 min on 8 host cores
 
+configs[1] is also stored for seeds 1-4 and in the deterministic mode (alpha 0, no noise, the
+action the argmax of the visits) -- the seeds and mode SURVEY.md 8d names for the parity runs.
+
 Inputs, as bench.py builds them (bench.random_roots + rng.predraw on RandomState(seed), global
 root order, then the rank's contiguous shard); weights tests/golden/weights_N{n}_s0.npz (the
 reference's MuZeroNet(TD_return=True) after torch.manual_seed(0), identical to bench.py's
@@ -37,6 +40,16 @@ CONFIGS = {
 }
 SEED = 0
 BLOCK = 256
+# further draws of configs[1] (seeds 0..4; the parity runs' deterministic mode with alpha 0):
+# tag: (config tag, seed, deterministic)
+VARIANTS = {f"c1_4096_s{k}": ("c1_4096", k, False) for k in range(1, 5)}
+VARIANTS["c1_4096_det"] = ("c1_4096", 0, True)
+
+
+def _spec(tag):
+    """(n, global roots, sims, world, rank, seed, deterministic) of a fixture tag"""
+    base, seed, det = VARIANTS.get(tag, (tag, SEED, False))
+    return (*CONFIGS[base], seed, det)
 
 
 def inputs(tag):
@@ -45,16 +58,21 @@ def inputs(tag):
     from muzero_hanoi_amd import distributed as mdist
     from muzero_hanoi_amd import rng
 
-    n, GB, S, W, r = CONFIGS[tag]
-    obs = bench.random_roots(n, GB, SEED)
-    noise, tie, u = rng.predraw(GB, deterministic=False, alpha=0.25, rng=np.random.RandomState(SEED))
-    return tuple(np.ascontiguousarray(mdist.shard(x, W, r)) for x in (obs, noise, tie, u))
+    n, GB, S, W, r, seed, det = _spec(tag)
+    obs = bench.random_roots(n, GB, seed)
+    noise, tie, u = rng.predraw(GB, deterministic=det, alpha=0.0 if det else 0.25, rng=np.random.RandomState(seed))
+    return tuple(None if x is None else np.ascontiguousarray(mdist.shard(x, W, r)) for x in (obs, noise, tie, u))
+
+
+def deterministic(tag):
+    return _spec(tag)[6]
 
 
 def inputs_sha(obs, noise, tie, u):
     h = hashlib.sha256()
-    for x in (obs.astype(np.float32), noise.astype(np.float64), tie.astype(np.int32), u.astype(np.float64)):
-        h.update(np.ascontiguousarray(x).tobytes())
+    for x, t in ((obs, np.float32), (noise, np.float64), (tie, np.int32), (u, np.float64)):
+        if x is not None:  # the deterministic mode draws no noise and no action uniform
+            h.update(np.ascontiguousarray(x, t).tobytes())
     return np.frombuffer(h.digest(), np.uint8)
 
 
@@ -78,19 +96,19 @@ def weights(n):
 
 
 def _chunk(args):
-    n, S, obs, noise, tie, u = args
+    n, S, obs, noise, tie, u, det = args
     from oracle import oracle
 
     flat, sup = weights(n)
     r = oracle.search(n, S, obs, flat=flat, support=sup, noise=noise, tie_idx=tie, action_u=u, temperature=1.0,
-                      deterministic=False, discount=0.8)
+                      deterministic=det, discount=0.8)
     return {k: r[k] for k in ("visits", "rootQ", "mm_max", "mm_min", "action", "sel_steps", "extra_ties")}
 
 
 def generate(tag, procs):
     import torch
 
-    n, GB, S, W, r = CONFIGS[tag]
+    n, GB, S, W, r, seed, det = _spec(tag)
     obs, noise, tie, u = inputs(tag)
     B = len(obs)
     # bench.py's network is MuZeroNet after torch.manual_seed(0): the same weights as the fixture
@@ -101,13 +119,14 @@ def generate(tag, procs):
     net = MuZeroNet(3 * n, 6, 0.002, "cpu", TD_return=True)
     assert np.array_equal(engine.flat_weights(net.state_dict()), weights(n)[0]), "bench weights != fixture weights"
     step = 512
-    jobs = [(n, S, obs[i:i + step], noise[i:i + step], tie[i:i + step], u[i:i + step]) for i in range(0, B, step)]
+    sl = lambda x, i: None if x is None else x[i:i + step]
+    jobs = [(n, S, obs[i:i + step], sl(noise, i), tie[i:i + step], sl(u, i), det) for i in range(0, B, step)]
     with mp.get_context("spawn").Pool(procs) as pool:
         parts = pool.map(_chunk, jobs)
     cat = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
     mm = np.stack([cat["mm_max"], cat["mm_min"]], 1)
     assert cat["sel_steps"].max() < 65536 and cat["visits"].max() < 256
-    out = dict(n_disks=n, n_sims=S, global_roots=GB, world=W, rank=r, seed=SEED,
+    out = dict(n_disks=n, n_sims=S, global_roots=GB, world=W, rank=r, seed=seed, deterministic=det,
                visits=cat["visits"].astype(np.uint8), action=cat["action"].astype(np.uint8),
                sel_steps=cat["sel_steps"].astype(np.uint16), extra_ties=cat["extra_ties"].astype(np.uint8),
                rootq_minmax_sha=block_sha(cat["rootQ"], mm), inputs_sha=inputs_sha(obs, noise, tie, u))
@@ -118,7 +137,7 @@ def generate(tag, procs):
 
 
 if __name__ == "__main__":
-    tags = sys.argv[1:] or list(CONFIGS)
+    tags = sys.argv[1:] or list(CONFIGS) + list(VARIANTS)
     procs = min(8, os.cpu_count() or 1)
     for t in tags:
         generate(t, procs)

@@ -22,7 +22,8 @@ def gf():
     return gen_fullbatch
 
 
-@pytest.mark.parametrize("tag", ["c1_4096", "c3_16384", "c2_65536", "c4_shard0of8", "c2_shard7of8"])
+@pytest.mark.parametrize("tag", ["c1_4096", "c3_16384", "c2_65536", "c4_shard0of8", "c2_shard7of8", "c1_4096_s1",
+                                 "c1_4096_s2", "c1_4096_s3", "c1_4096_s4", "c1_4096_det"])
 def test_full_batch_fixture(gf, oracle, tag):
     z = golden(f"full_{tag}.npz")
     n, S = int(z["n_disks"]), int(z["n_sims"])
@@ -35,8 +36,9 @@ def test_full_batch_fixture(gf, oracle, tag):
     # so the sampled roots are checked field by field (visits, action, selection steps)
     idx = np.r_[0:2, B - 2:B]
     flat, sup = gf.weights(n)
-    r = oracle.search(n, S, obs[idx], flat=flat, support=sup, noise=noise[idx], tie_idx=tie[idx], action_u=u[idx],
-                      temperature=1.0, deterministic=False, discount=0.8)
+    sel = lambda x: None if x is None else x[idx]
+    r = oracle.search(n, S, obs[idx], flat=flat, support=sup, noise=sel(noise), tie_idx=tie[idx], action_u=sel(u),
+                      temperature=1.0, deterministic=gf.deterministic(tag), discount=0.8)
     assert np.array_equal(r["visits"], z["visits"][idx].astype(np.int32))
     assert np.array_equal(r["action"], z["action"][idx].astype(np.int32))
     assert np.array_equal(r["sel_steps"], z["sel_steps"][idx].astype(np.int64))

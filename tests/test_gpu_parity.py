@@ -515,7 +515,9 @@ def test_search_caller_bounds_instantiation(mzh, oracle, B, tile):
 
 # ------------------------------------------------- whole-batch oracle parity at BASELINE sizes
 FULL_BATCH = [("c1_4096", None), ("c3_16384", None), ("c2_65536", None), ("c4_shard0of8", None),
-              ("c2_shard7of8", None), ("c2_shard7of8", "occ2"), ("c2_shard7of8", "coop"), ("c1_4096", "occ2")]
+              ("c2_shard7of8", None), ("c2_shard7of8", "occ2"), ("c2_shard7of8", "coop"), ("c1_4096", "occ2"),
+              ("c1_4096_s1", None), ("c1_4096_s2", None), ("c1_4096_s3", None), ("c1_4096_s4", None),
+              ("c1_4096_det", None), ("c1_4096_det", "wave16")]
 
 
 def _first_diff(a, b):
@@ -530,7 +532,8 @@ def test_search_full_batch_equals_oracle(mzh, tag, kernel):
     shard at N=8, 32,768 7-disk roots x 100 sims), on bench.py's own inputs and reference-order
     draws, through the kernel the library picks, equals the C oracle's whole-batch outputs
     (tests/golden/gen_fullbatch.py; MCTS/mcts.py:34-126): visits, action, selection steps and extra
-    ties root by root, root Q and MinMaxStats bit for bit through per-256-root SHA-256 digests."""
+    ties root by root, root Q and MinMaxStats bit for bit through per-256-root SHA-256 digests.
+    configs[1] also for seeds 1-4 and in the deterministic mode (alpha 0, argmax action)."""
     import sys
 
     sys.path.insert(0, GOLDEN)
@@ -543,9 +546,9 @@ def test_search_full_batch_equals_oracle(mzh, tag, kernel):
     flat, sup = gf.weights(n)
     B = len(obs)
     eng = _engine(mzh, n, S, B, sup, flat)
-    tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
+    tt = lambda a: None if a is None else torch.tensor(np.asarray(a), device=DEV)
     o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0,
-                   deterministic=False, discount=0.8, eps=0.25, kernel=kernel)
+                   deterministic=gf.deterministic(tag), discount=0.8, eps=0.25, kernel=kernel)
     kern = o["_plan"]["kernel"]
     if kernel == "occ2":
         assert kern.startswith("mzh_search_occ2_kernel<"), kern
