@@ -38,6 +38,9 @@ CONFIGS = {
     "c2_shard7of8": (4, 65536, 50, 8, 7),    # configs[2], rank 7's 8,192-root shard at N=8 (the 8-GPU headline)
     "c4_shard0of8": (7, 262144, 100, 8, 0),  # configs[4], rank 0's 32,768-root shard at N=8
 }
+# configs[4]'s other seven shards: with rank 0's, every root of the 262,144-root batch (the GPU test
+# runs the whole batch as one launch and compares it with the eight shards' outputs in root order)
+CONFIGS.update({f"c4_shard{r}of8": (7, 262144, 100, 8, r) for r in range(1, 8)})
 SEED = 0
 BLOCK = 256
 # further draws of configs[1] (seeds 0..4; the parity runs' deterministic mode with alpha 0):

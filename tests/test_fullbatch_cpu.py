@@ -22,8 +22,16 @@ def gf():
     return gen_fullbatch
 
 
-@pytest.mark.parametrize("tag", ["c1_4096", "c3_16384", "c2_65536", "c4_shard0of8", "c2_shard7of8", "c1_4096_s1",
-                                 "c1_4096_s2", "c1_4096_s3", "c1_4096_s4", "c1_4096_det"])
+TAGS = sorted(f[len("full_"):-len(".npz")] for f in os.listdir(GOLDEN) if f.startswith("full_") and f.endswith(".npz"))
+
+
+def test_every_config_has_its_fixture():
+    import gen_fullbatch as gf
+
+    assert sorted(list(gf.CONFIGS) + list(gf.VARIANTS)) == TAGS
+
+
+@pytest.mark.parametrize("tag", TAGS)
 def test_full_batch_fixture(gf, oracle, tag):
     z = golden(f"full_{tag}.npz")
     n, S = int(z["n_disks"]), int(z["n_sims"])

@@ -565,6 +565,41 @@ def test_search_full_batch_equals_oracle(mzh, tag, kernel):
         assert np.array_equal(o["root_q"], z["root_q"]) and np.array_equal(o["minmax"], z["minmax"])
 
 
+def test_search_configs4_whole_batch_equals_oracle(mzh):
+    """configs[4] (7 disks, 262,144 roots, 100 sims) as ONE launch on one GPU (the wave kernel), every root
+    against the C oracle: the eight N=8 shard fixtures (full_c4_shard{0..7}of8.npz) hold the oracle's
+    outputs for all 262,144 roots in root order (MCTS/mcts.py:34-126)."""
+    import sys
+
+    sys.path.insert(0, GOLDEN)
+    import gen_fullbatch as gf
+
+    tags = [f"c4_shard{r}of8" for r in range(8)]
+    parts = [gf.inputs(t) for t in tags]
+    obs, noise, tie, u = (np.concatenate([p[i] for p in parts]) for i in range(4))
+    zs = [golden(f"full_{t}.npz") for t in tags]
+    n, S = int(zs[0]["n_disks"]), int(zs[0]["n_sims"])
+    flat, sup = gf.weights(n)
+    B = len(obs)
+    assert B == 262144
+    eng = _engine(mzh, n, S, B, sup, flat)
+    tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
+    o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0,
+                   deterministic=False, discount=0.8, eps=0.25)
+    kern = o["_plan"]["kernel"]
+    o = {k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")}
+    eng.close()
+    b = B // 8
+    for r, (t, z) in enumerate(zip(tags, zs)):
+        sl = slice(r * b, (r + 1) * b)
+        for k, want in (("visits", z["visits"]), ("action", z["action"]), ("sel_steps", z["sel_steps"]),
+                        ("extra_ties", z["extra_ties"])):
+            d = _first_diff(o[k][sl].astype(np.int64), want.astype(np.int64))
+            assert d is None, f"{t} ({kern}): {k} differs at root {r * b + d[0]} ({d[1]} roots)"
+        d = _first_diff(gf.block_sha(o["root_q"][sl], o["minmax"][sl]), z["rootq_minmax_sha"])
+        assert d is None, f"{t} ({kern}): root Q / MinMaxStats differ in 256-root block {d[0]} of the shard"
+
+
 @pytest.mark.parametrize("kernel,tile", [("coop", 16), ("coop", 32), ("occ2", None), ("wave", None), ("wave16", None)])
 def test_search_lockstep_levels(mzh, oracle, kernel, tile):
     """mzh_search_args.lockstep_levels (the select/backup latency model's input, bench.tree_latency_model):
