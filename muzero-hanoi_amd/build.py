@@ -25,6 +25,11 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MZH_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off",
          "-Wall", "-Wno-unused-result", "-I", os.path.join(REPO, "include")]
+# per-source additions.  mzh_search.hip (the cooperative kernels, one wave per SIMD at 256 arch VGPRs):
+# MFMA accumulators in arch VGPRs instead of the heuristic's AGPRs, so no epilogue element needs a
+# v_accvgpr_read (8,192 roots -1.7%, 4,096 -2.0%; the wave kernels, built without it, measured neutral;
+# profiles/r05_vgpr_form_ab.json).  Register allocation only: the same instructions, bit-identical results.
+SOURCE_FLAGS = {"mzh_search.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 
 
 BUILD_ID_MARKER = b"MZH_BUILD_ID:"
@@ -47,6 +52,8 @@ def source_hash(flags=None):
     # flags without the checkout's absolute path (the GPU box runs the same tree from another path)
     h.update(" ".join(FLAGS if flags is None else flags).replace(REPO, "<repo>").encode())
     h.update(" ".join(HOST_FLAGS).encode())
+    for src in sorted(SOURCE_FLAGS):
+        h.update(f"{src}:{' '.join(SOURCE_FLAGS[src])}".encode())
     return h.hexdigest()[:20]
 
 
@@ -93,7 +100,7 @@ def build(verbose=False, force=False, diag=False, tag="", defines=()):
         s = os.path.join(CSRC, src)
         o = os.path.join(obj_dir, src.replace(".hip", ".o"))
         if force or _stale(o, [s] + headers):
-            jobs.append([HIPCC, *flags, "-c", s, "-o", o])
+            jobs.append([HIPCC, *flags, *SOURCE_FLAGS.get(src, []), "-c", s, "-o", o])
     for src in HOST_SOURCES:
         s = os.path.join(CSRC, src)
         o = os.path.join(obj_dir, src.replace(".cpp", ".host.o"))

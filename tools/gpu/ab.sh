@@ -4,7 +4,7 @@ set -e
 mkdir -p gpurun_out
 LIBS=$1; shift
 B="timeout -k 10 300 python bench.py --no-cpu-baseline --no-tree --no-minmax-leg --steps 10 --warmup 2"
-for rep in 1 2; do
+for rep in ${AB_REPS:-1 2}; do
   for lib in $LIBS; do
     L=""; [ $lib != libmzh ] && L="MZH_LIB=$PWD/muzero-hanoi_amd/$lib.so"
     for w in "$@"; do
