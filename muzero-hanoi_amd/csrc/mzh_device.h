@@ -578,30 +578,35 @@ __device__ __forceinline__ void mzh_mma_store(floatx4* f, float* bv, const MzhCh
 #pragma unroll
       for (int i = 0; i < 4; ++i) acts[m * 4 + i] = act[m * 16 + g * 4 + i];
   }
+  // LDS addresses as one lane base per row (gather) or per tile (epilogue) plus compile-time element
+  // offsets, so every ds_read / ds_write takes its offset as an immediate: an index added before the
+  // byte scaling cost two VALU per element (v_add_u32 + v_lshl_add_u32) -- ~290 a wave and simulation
+  // at 32 roots, each an issue slot of the MFMA stream.  The one-hot chunk's tiles are consecutive
+  // (mzh_chunk: col0[q] = col0[0] + 16q).
   auto gather_oh = [&]() {
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float* ohrow = oht + acts[m * 4 + i] * MZH_F + r;
+        const float* ohrow = oht + acts[m * 4 + i] * MZH_F + (c.col0[0] + r);
 #pragma unroll
-        for (int q = 0; q < NJ; ++q) oh[(q * MT + m) * 4 + i] = ohrow[c.col0[q]];
+        for (int q = 0; q < NJ; ++q) oh[(q * MT + m) * 4 + i] = ohrow[16 * q];
       }
   };
   auto epilogue = [&](int q) {
     // output column col0 + r; a hidden / latent unit is stored at its k-block-order position
     const int pos = c.col0[q] + (NAT ? r : 4 * (r & 3) + (r >> 2));
     if ((ALL || q < c.nj) && (!NAT || pos < c.ldo)) {
+      float* ob = c.out[q] + (g * 4 * c.ldo + pos);  // row g * 4 of row tile 0
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int row = m * 16 + g * 4 + i;
           float v = acc[q][m][i];
           if (oht) v = v + oh[(q * MT + m) * 4 + i];
           v = v + bv[q];
           if (relu) v = v > 0.0f ? v : 0.0f;
-          c.out[q][row * c.ldo + pos] = v;
+          ob[(m * 16 + i) * c.ldo] = v;
         }
       }
     }
