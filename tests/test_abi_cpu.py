@@ -134,6 +134,9 @@ def test_build_id_names_the_checked_out_sources(lib, tmp_path, monkeypatch):
     # the GPU box runs the tree from another path: the checkout path is not part of the id
     monkeypatch.undo()
     assert build.source_hash([f.replace(build.REPO, "<repo>") for f in build.FLAGS]) == want
+    # per-source flags (build.SOURCE_FLAGS: the cooperative kernels' register form) are part of the id too
+    monkeypatch.setattr(build, "SOURCE_FLAGS", {k: [] for k in build.SOURCE_FLAGS})
+    assert build.source_hash() != want
 
 
 def test_train_args_layout_matches_header(lib, tmp_path):
