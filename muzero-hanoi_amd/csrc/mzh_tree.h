@@ -356,13 +356,21 @@ struct MzhTree {
     for (int jj = 0; jj < DC; ++jj) Rj[jj] = st.pc[r][jj].R;
     MZH_STAMP_DECL
     if (!REPLAY) {
-      // the new node's latent (read back when one of its children is expanded -- usually
-      // within a few simulations on the deepening path, so it stays cacheable)
+      // the new node's latent (read back when one of its children is expanded)
       const float* src = &sm.x[r * MZH_LD64 + c * 8];
-      floatx4* dst = reinterpret_cast<floatx4*>(p.htree) + ((size_t)(root0 + r) * p.E + enew) * 16 + c * 2;
       const floatx4 v0 = {src[0], src[1], src[2], src[3]}, v1 = {src[4], src[5], src[6], src[7]};
-      dst[0] = v0;
-      dst[1] = v1;
+      {
+        // the new node's latent is written through and not kept in the XCD's L2 (cache policy 16 = sc1):
+        // at 32 roots a CU it would displace the tree blocks the next selections walk (the parent-latent
+        // gather then reads it from the MALL).  8,192 roots -0.6%, 4,096 -1.1% (plain stores kept in L2;
+        // the `nt` policy +1.3% / +0.7%, profiles/r05_coop_ab.json).  Workgroup-uniform base, the lane's
+        // byte offset in a VGPR.
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const __amdgpu_buffer_rsrc_t lr = mzh_rsrc(reinterpret_cast<floatx4*>(p.htree) + (size_t)root0 * p.E * 16);
+        const int vo = ((r * p.E + enew) * 16 + c * 2) * 16;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v0), lr, vo, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v1), lr, vo + 16, 0, 16);
+      }
     }
     MzhBlock* nb = tb + enew;  // the new expanded node's 6 children (node.py:44-49)
     if (c < MZH_A) {
