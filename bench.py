@@ -81,6 +81,55 @@ def root_flops(n_disks):
     return 2 * (768 * n_disks + 59_136)  # initial_inference matmul FLOPs
 
 
+def launch_stats(ms):
+    """per-launch HIP-event times -> min / median / max / mean; the line prices `frac` on the median so one
+    slow or fast launch (in-run clock drift) does not move it"""
+    a = np.asarray(ms, np.float64)
+    return {"n": int(a.size), "min": float(a.min()), "median": float(np.median(a)), "max": float(a.max()),
+            "mean": float(a.mean())}
+
+
+def abba_order(rounds):
+    """launch order of an A/B comparison taken in one window: A B B A per round, so neither leg always
+    follows the other (the same clocks and the same predecessor mix for both)"""
+    return [x for _ in range(rounds) for x in (0, 1, 1, 0)]
+
+
+def ab_summary(ta, tb):
+    """two legs timed in one ABBA window: each leg's launch_stats and the ratio of their medians"""
+    sa, sb = launch_stats(ta), launch_stats(tb)
+    return {"a": sa, "b": sb, "ratio_median": sb["median"] / sa["median"]}
+
+
+def device_identity(dev):
+    """what identifies this rank's GPU in a multi-GPU record: LOCAL_RANK, host, and the device's UUID / PCI
+    location as torch reports them (fields torch does not have on this build are left out)"""
+    import socket
+
+    props = torch.cuda.get_device_properties(dev)
+    ident = {"local_rank": int(os.environ.get("LOCAL_RANK", "0")), "host": socket.gethostname(),
+             "device_index": dev.index, "name": props.name}
+    for k in ("uuid", "pci_bus_id", "pci_device_id", "pci_domain_id"):
+        v = getattr(props, k, None)
+        if v is not None:
+            ident[k] = str(v)
+    return ident
+
+
+def distinct_devices(idents):
+    """physical GPUs among the ranks' identities: (host, UUID) when torch reports a UUID, else (host, PCI
+    domain / bus / device), else (host, device index)"""
+    keys = set()
+    for d in idents:
+        if "uuid" in d:
+            keys.add((d["host"], d["uuid"]))
+        elif "pci_bus_id" in d:
+            keys.add((d["host"], d.get("pci_domain_id"), d["pci_bus_id"], d.get("pci_device_id")))
+        else:
+            keys.add((d["host"], d.get("device_index")))
+    return len(keys)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -503,6 +552,8 @@ def main():
     # kernel-time probe: HIP events on the launch stream around each search launch
     plan = search_plan(S, B, a.kernel, a.tile)
     assert out["_plan"]["kernel"] == plan["kernel"], (out["_plan"], plan)  # the query names what launched
+    if a.kernel == "occ2":
+        assert plan["kernel"].startswith("mzh_search_occ2_kernel<"), plan  # --kernel occ2 measures occ2
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     gevs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
     if dist is not None:
@@ -526,7 +577,8 @@ def main():
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+    kstats = launch_stats([s.elapsed_time(e) for s, e in evs])
+    kern_ms = kstats["median"]
     gather_ms = None
     if overlap:
         # what one gather costs on its own (untimed probe after the loop: HIP events around a synchronous one)
@@ -554,21 +606,26 @@ def main():
         search_mm()
         torch.cuda.synchronize(dev)
         assert torch.equal(mout["visits"], out["visits"]), "fresh caller bounds changed the search"
-        # alternated with the plain search, so both see the same clocks
-        mev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(2)]
-               for _ in range(5)]
-        for pair in mev:
-            for fn, (s_, e_) in zip((search, search_mm), pair):
-                s_.record(stream)
-                fn()
-                e_.record(stream)
+        # A B B A with the plain search in one window, so both legs see the same clocks and neither always
+        # runs after the other (round 5's 5 alternated pairs read the plain kernel 3% slower than the
+        # 20-step loop: a drift artefact in the ratio)
+        order = abba_order(4)
+        mev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in order]
+        for leg, (s_, e_) in zip(order, mev):
+            s_.record(stream)
+            (search, search_mm)[leg]()
+            e_.record(stream)
         torch.cuda.synchronize(dev)
-        t_plain = float(np.mean([p[0][0].elapsed_time(p[0][1]) for p in mev]))
-        t_mm = float(np.mean([p[1][0].elapsed_time(p[1][1]) for p in mev]))
-        mm = {"kernel": mout["_plan"]["kernel"], "kernel_ms": t_mm, "plain_kernel_ms_alternated": t_plain,
-              "ratio": t_mm / t_plain,
+        legs = ([], [])
+        for leg, (s_, e_) in zip(order, mev):
+            legs[leg].append(s_.elapsed_time(e_))
+        ab = ab_summary(*legs)
+        mm = {"kernel": mout["_plan"]["kernel"], "kernel_ms": ab["b"]["median"],
+              "plain_kernel_ms_same_window": ab["a"]["median"], "ratio": ab["ratio_median"],
+              "launch_stats": ab["b"], "plain_launch_stats": ab["a"],
               "what": "the same search with minmax_in given (fresh bounds: identical visits), the instantiation "
-                      "MCTS.run_mcts and batched self-play launch; 5 launches alternated with 5 plain ones, HIP events"}
+                      "MCTS.run_mcts and batched self-play launch; 8 launches interleaved A B B A with 8 plain ones "
+                      "in one window, HIP events, medians"}
 
     # select / expand / backup alone: the replay instantiation of the same kernel on the same roots,
     # network outputs drawn like a random-init network's (near-uniform priors, small values)
@@ -603,10 +660,12 @@ def main():
             replay()
             e_.record(stream)
         torch.cuda.synchronize(dev)
-        tree_ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in tev]))
+        tstats = launch_stats([s_.elapsed_time(e_) for s_, e_ in tev])
+        tree_ms = tstats["median"]
         tb = tree_bytes(rsel, B, S, EXPAND_BYTES_REPLAY)
         tree = {"bound": "hbm", "kernel": rout["_plan"]["kernel"],
-                "bytes_per_launch": tb, "kernel_ms": tree_ms, "achieved": tb / (tree_ms * 1e-3) / 1e9,
+                "bytes_per_launch": tb, "kernel_ms": tree_ms, "launch_stats": tstats,
+                "achieved": tb / (tree_ms * 1e-3) / 1e9,
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s", "sel_steps_per_sim": rsel / (B * S),
                 "frac": tb / (tree_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "traffic": None,
                 "fused_tree_bytes_per_launch": tree_bytes(sel_sum, B, S, EXPAND_BYTES),
@@ -635,7 +694,10 @@ def main():
         allr = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
         dist.all_gather(allr, mine)
         allr = torch.stack(allr).cpu().numpy()
+        idents = [None] * dist.get_world_size()
+        dist.all_gather_object(idents, dict(device_identity(dev), rank=rank))
         dinfo = {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()),
+                 "devices": idents, "distinct_devices": distinct_devices(idents),
                  "gather_ms_per_step": {"max": float(allr[:, 3].max()), "min": float(allr[:, 3].min())} if gather else None,
                  "kernel_ms_per_rank": [float(x) for x in allr[:, 1]],
                  "roots_per_rank": [int(x) for x in allr[:, 4]],
@@ -672,7 +734,13 @@ def main():
         tree["traffic"] = tent.get("tree_hbm_bytes_per_launch")
         if tent.get("tree_issue_frac") is not None:
             # the issue ceiling: the fraction of the SIMDs' cycles some wave issued (PMC of this build)
+            twps = waves_per_simd(rout["_plan"], B)
             tree["issue"] = {"frac": tent["tree_issue_frac"], "waitcnt_frac": tent.get("tree_waitcnt_frac"),
+                             "waves_per_simd": twps, "upper_bound": twps > 1,
+                             "note": "SQ_ACTIVE_INST_ANY sums per-wave issue cycles over waves: with two waves per "
+                                     "SIMD their overlapping issue is counted twice, so frac is an upper bound of "
+                                     "the SIMDs' issue-busy fraction there" if twps > 1 else
+                                     "one wave per SIMD: the SIMDs' issue-busy fraction",
                              "source": "rocprofv3 --pmc SQ_ACTIVE_INST_ANY x 4 / (1,024 SIMDs x GRBM_GUI_ACTIVE / 8) "
                                        "of this build (tools/prof.sh + tools/traffic.py)"}
             tree["binding"]["fracs"]["issue"] = tent["tree_issue_frac"]
@@ -708,7 +776,9 @@ def main():
                      "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_source": {"key": tkey, "note": tnote,
                                         "kernel_avg_ns_profiled": tent.get("avg_ns") if tent else None},
-                     "kernel": kname, "kernel_ms": kern_ms,
+                     "kernel": kname, "kernel_ms": kern_ms, "launch_stats": kstats,
+                     "kernel_ms_what": "median of the timed launches' HIP-event times (this rank; max over ranks "
+                                       "at N > 1); achieved and frac are priced on it",
                      "flop_per_launch": flops_launch, "sel_steps_per_sim": sel_sum / (B * S),
                      "measured_ceiling": {"value": FP32_MFMA_MEASURED_TFLOPS[wps],
                                           "frac": achieved / FP32_MFMA_MEASURED_TFLOPS[wps],
@@ -742,11 +812,17 @@ def dry_run(a, world, rank, GB, S, N):
         import torch.distributed as dist
 
         dist.init_process_group(a.dist_backend)
+        import socket
+
         mine = torch.tensor([float(rank), float(shards[rank][1] - shards[rank][0])], dtype=torch.float64)
         allr = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
         dist.all_gather(allr, mine)
+        idents = [None] * dist.get_world_size()
+        dist.all_gather_object(idents, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                                        "host": socket.gethostname()})
         dinfo = {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()),
-                 "ranks": [int(x[0]) for x in allr], "roots_per_rank": [int(x[1]) for x in allr]}
+                 "ranks": [int(x[0]) for x in allr], "roots_per_rank": [int(x[1]) for x in allr],
+                 "devices": idents}
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "steps": a.steps, "warmup": a.warmup,

@@ -48,7 +48,10 @@ extern "C" {
 #define MZH_FLAG_COOP_TILE16 16u /* cooperative kernel: 16 roots per workgroup (default for B <= 4096) */
 #define MZH_FLAG_COOP_TILE32 32u /* cooperative kernel: 32 roots per workgroup (default for B > 4096) */
 #define MZH_FLAG_COOP_OCC2 64u /* cooperative kernel, 16-root tiles, two workgroups per CU
-                                  (mzh_search_occ2_kernel; MLP searches whose LDS fits twice per CU) */
+                                  (mzh_search_occ2_kernel).  An MLP search whose LDS does not fit twice per
+                                  CU fails with MZH_ERR_CAPACITY; a replay (tree-only) search, which has no
+                                  occ2 instantiation, runs the cooperative replay kernel instead (the plan
+                                  names it) */
 
 typedef struct mzh_engine mzh_engine;
 typedef void* mzh_stream; /* hipStream_t */

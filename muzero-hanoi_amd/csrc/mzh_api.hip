@@ -499,8 +499,12 @@ static int make_plan(int B, int S, uint32_t flags, bool replay, int support, boo
   } else {
     q.R = pick_tile(B, flags);
     // the two-workgroups-per-CU 16-root kernel: forced by MZH_FLAG_COOP_OCC2 (MLP searches; its LDS must
-    // leave room for the second workgroup)
-    if ((flags & MZH_FLAG_COOP_OCC2) && !replay && 2 * mzh_search_smem_bytes(16, S, false, true) <= kMaxLds) {
+    // leave room for the second workgroup -- a search it cannot serve is an error, never a silent fallback;
+    // replay searches have no occ2 instantiation and take the cooperative replay kernel, as mzh.h says)
+    if ((flags & MZH_FLAG_COOP_OCC2) && !replay && 2 * mzh_search_smem_bytes(16, S, false, true) > kMaxLds)
+      return fail(MZH_ERR_CAPACITY, "MZH_FLAG_COOP_OCC2: n_sims=%d needs %zu B of LDS per workgroup, more than "
+                  "half a CU's", S, mzh_search_smem_bytes(16, S, false, true));
+    if ((flags & MZH_FLAG_COOP_OCC2) && !replay) {
       q.R = 16;
       q.occ2 = 1;
       q.ohl = 0;

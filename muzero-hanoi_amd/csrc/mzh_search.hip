@@ -150,26 +150,29 @@ __device__ __forceinline__ void mzh_search_body(const MzhNet& net, const MzhSear
   if (town) rs.load(st, tr);
 
   // p.lockstep_levels: the workgroup's deepest selection below the root per simulation (every wave's
-  // maximum through LDS, read by thread 0 after the simulation's closing barrier)
+  // maximum through LDS, read by thread 0 after the simulation's closing barrier).  Selection k writes
+  // slot k & 1: without an MLP (replay) the other waves may finish selection k + 1 before thread 0 has
+  // read selection k's maxima, but selection k + 2 -- the next writer of that slot -- starts only after
+  // the barrier that thread 0 reaches once it has read them
   const bool lcount = p.lockstep_levels != nullptr;
   int lsum = 0;
-  auto wave_level = [&]() {
+  auto wave_level = [&](int k) {
     int m = town ? rs.depth - 1 : 0;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off));
-    if (lane == 0) st.lvl[wave] = m;
+    if (lane == 0) st.lvl[k & 1][wave] = m;
   };
-  auto group_level = [&]() {
-    int m = st.lvl[0];
+  auto group_level = [&](int k) {
+    int m = st.lvl[k & 1][0];
 #pragma unroll
-    for (int w = 1; w < MZH_WAVES; ++w) m = max(m, st.lvl[w]);
+    for (int w = 1; w < MZH_WAVES; ++w) m = max(m, st.lvl[k & 1][w]);
     lsum += m;
   };
   MZH_STAMP_DECL
   if (town) tree.template select<MMIN>(tr, tc, 0, rs);
-  if (lcount) wave_level();
+  if (lcount) wave_level(0);
   __syncthreads();
-  if (lcount && tid == 0 && S > 0) group_level();
+  if (lcount && tid == 0 && S > 0) group_level(0);
   for (int s = 0; s < S; ++s) {
     // ---------------- expand via the network (mcts.py:88-106) ----------------
     if (!REPLAY) {
@@ -204,9 +207,9 @@ __device__ __forceinline__ void mzh_search_body(const MzhNet& net, const MzhSear
         MZH_STAMP(30);
       }
     }
-    if (lcount && s + 1 < S) wave_level();
+    if (lcount && s + 1 < S) wave_level(s + 1);
     __syncthreads();
-    if (lcount && tid == 0 && s + 1 < S) group_level();
+    if (lcount && tid == 0 && s + 1 < S) group_level(s + 1);
     MZH_STAMP(23);
   }
   if (lcount && tid == 0) p.lockstep_levels[blockIdx.x] = lsum;

@@ -64,7 +64,7 @@ struct SearchSmem {
   int leafA[R];
   int steps[R];
   int tie[R];  // the host-drawn index for the first 6-way tie (tie_idx)
-  int lvl[MZH_WAVES];  // p.lockstep_levels: each wave's deepest selection of the current simulation
+  int lvl[2][MZH_WAVES];  // p.lockstep_levels: each wave's deepest selection, by selection parity
 };
 
 // a / b correctly rounded from y = RN(1/b) (Markstein: q = RN(a*y) is within one ulp, the fma

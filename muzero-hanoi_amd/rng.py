@@ -93,19 +93,22 @@ def _predraw_c(rs, n_roots, *, deterministic, alpha, eps, draw_action):
     u = np.empty(n_roots, np.float64) if (not deterministic and draw_action) else None
     # the gamma sampler uses the polar Gaussian (and the RandomState's cached deviate) only for alpha > 1
     gauss_used = noisy and float(alphas[0]) > 1.0
-    if gauss_used:
-        st = rs.get_state()
-        g = np.array([float(st[3]), st[4]], np.float64)
-    else:
-        g = np.zeros(2, np.float64)
-    addr = rs._bit_generator.ctypes.state_address
     p = lambda x: None if x is None else x.ctypes.data_as(ctypes.c_void_p)
-    status = L.mzh_rng_predraw(ctypes.c_void_p(addr), p(g), int(n_roots), 6 if noisy else 0, p(alphas), 6,
-                               1 if u is not None else 0, p(noise), p(tie), p(u))
-    _lib.check(status, "mzh_rng_predraw")
-    if gauss_used:
-        st = rs.get_state()  # the key / pos the C code advanced in place, with the new Gaussian cache
-        rs.set_state((st[0], st[1], st[2], int(g[0]), float(g[1])))
+    # the bit generator's own lock (every RandomState method takes it): a NumPy draw on the same stream
+    # from another thread cannot interleave with the in-place C loop
+    with rs._bit_generator.lock:
+        if gauss_used:
+            st = rs.get_state()
+            g = np.array([float(st[3]), st[4]], np.float64)
+        else:
+            g = np.zeros(2, np.float64)
+        addr = rs._bit_generator.ctypes.state_address
+        status = L.mzh_rng_predraw(ctypes.c_void_p(addr), p(g), int(n_roots), 6 if noisy else 0, p(alphas), 6,
+                                   1 if u is not None else 0, p(noise), p(tie), p(u))
+        _lib.check(status, "mzh_rng_predraw")
+        if gauss_used:
+            st = rs.get_state()  # the key / pos the C code advanced in place, with the new Gaussian cache
+            rs.set_state((st[0], st[1], st[2], int(g[0]), float(g[1])))
     return noise, tie, u
 
 

@@ -461,7 +461,7 @@ typedef struct {
 static void search_one(int S, double discount, int flags, const orc_net* net, const float* obs,
                        const double* noise, double eps, int tie_idx, const double* table,
                        orc_minmax* mm, orc_node* nodes, float* hbuf, int* visits, double* rootQ,
-                       int* extra_ties, int* latent, int* latent_len, long* sel_steps) {
+                       int* extra_ties, int* latent, int* latent_len, long* sel_steps, int* depths) {
   int n_nodes = 0;
   int n_h = 0;
   float root_pi[ORC_A];
@@ -540,6 +540,7 @@ static void search_one(int S, double discount, int flags, const orc_net* net, co
       steps++;
     }
     if (latent_len && s == S - 1) *latent_len = depth;
+    if (depths) depths[s] = depth; /* this simulation's selection depth (levels below the root + 1) */
     /* Phase 2: expand leaf from parent's latent and the leaf's move (mcts.py:88-106) */
     orc_node* leaf = &nodes[node];
     orc_node* par = &nodes[leaf->parent];
@@ -624,14 +625,15 @@ int orc_play_policy(const int* visits, double temperature, int deterministic, do
 
 /* Batched search: B independent roots, each a fresh (or given) MinMaxStats.
  * Network = MLP (flat != NULL) or replay (rp_* != NULL).  All output pointers may be NULL
- * except visits. */
+ * except visits.  depths [B][S] (nullable): every simulation's selection depth, the input of the
+ * lockstep-grouping price (tools/price_grouping.py). */
 int orc_search(int n_disks, int S, int B, double discount, int flags, const float* flat,
                int support, const float* obs, const float* rp_root_pi, const float* rp_pi,
                const float* rp_rwd, const float* rp_val, const double* noise, double eps,
                const int* tie_idx, const double* action_u, double temperature, int deterministic,
                const double* powtab, const double* minmax_in, int* visits, double* rootQ, double* minmax_out,
                int* extra_ties, int* action, double* pi, int* latent, int* latent_len,
-               long* sel_steps) {
+               long* sel_steps, int* depths) {
   int in_dim = 3 * n_disks;
   orc_weights w;
   if (flat) bind_weights(&w, flat, in_dim, support);
@@ -659,7 +661,7 @@ int orc_search(int n_disks, int S, int B, double discount, int flags, const floa
     double q;
     search_one(S, discount, flags, &net, obs + (size_t)b * in_dim, noise ? noise + (size_t)b * ORC_A : NULL,
                eps, tie_idx ? tie_idx[b] : 0, table, &mm, nodes, hbuf, visits + (size_t)b * ORC_A, &q, &et,
-               latent ? latent + (size_t)b * (S + 1) : NULL, &ll, &st);
+               latent ? latent + (size_t)b * (S + 1) : NULL, &ll, &st, depths ? depths + (size_t)b * S : NULL);
     if (rootQ) rootQ[b] = q;
     if (minmax_out) { minmax_out[2 * b] = mm.maximum; minmax_out[2 * b + 1] = mm.minimum; }
     if (extra_ties) extra_ties[b] = et;

@@ -71,7 +71,7 @@ def lib():
             [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_void_p,
              ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p,
-             ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_void_p] * 9)
+             ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_void_p] * 10)
     return _lib
 
 
@@ -198,10 +198,11 @@ def play_policy(visits, temperature, deterministic, u=0.0):
 
 def search(n_disks, S, obs, *, flat=None, support=33, replay=None, noise=None, eps=0.25,
            tie_idx=None, action_u=None, temperature=1.0, deterministic=False, minmax_in=None,
-           discount=0.8, np1_ucb=False):
+           discount=0.8, np1_ucb=False, depths=False):
     """Batched search over B independent roots (each a fresh or given MinMaxStats).
 
-    replay: dict(root_pi[B,6], pi[B,S,6], rwd[B,S], value[B,S]) -> tree-only mode."""
+    replay: dict(root_pi[B,6], pi[B,S,6], rwd[B,S], value[B,S]) -> tree-only mode.
+    depths=True adds `depths` [B,S]: each simulation's selection depth."""
     obs = _c(obs, np.float32)
     B = obs.shape[0]
     visits = np.zeros((B, 6), np.int32)
@@ -213,6 +214,7 @@ def search(n_disks, S, obs, *, flat=None, support=33, replay=None, noise=None, e
     latent = np.full((B, S + 1), -1, np.int32)
     latent_len = np.zeros(B, np.int32)
     steps = np.zeros(B, np.int64)
+    dep = np.zeros((B, S), np.int32) if depths else None
     rp = [None] * 4
     if replay is not None:
         rp = [_c(replay["root_pi"], np.float32), _c(replay["pi"], np.float32),
@@ -227,10 +229,13 @@ def search(n_disks, S, obs, *, flat=None, support=33, replay=None, noise=None, e
                           _p(obs), _p(rp[0]), _p(rp[1]), _p(rp[2]), _p(rp[3]), _p(noise), float(eps),
                           _p(tie), _p(au), float(temperature), int(deterministic), _p(pt), _p(mmi),
                           _p(visits), _p(rootQ), _p(mm), _p(et), _p(action), _p(pi), _p(latent),
-                          _p(latent_len), _p(steps))
+                          _p(latent_len), _p(steps), _p(dep))
     if st == -2:
         raise ValueError(f"Expect `temperature` to be in the range [0.0, 1.0], got {temperature}")
     if st != 0:
         raise RuntimeError(f"orc_search failed: {st}")
-    return dict(visits=visits, rootQ=rootQ, mm_max=mm[:, 0], mm_min=mm[:, 1], extra_ties=et,
-                action=action, pi=pi, latent=latent, latent_len=latent_len, sel_steps=steps)
+    out = dict(visits=visits, rootQ=rootQ, mm_max=mm[:, 0], mm_min=mm[:, 1], extra_ties=et,
+               action=action, pi=pi, latent=latent, latent_len=latent_len, sel_steps=steps)
+    if depths:
+        out["depths"] = dep
+    return out

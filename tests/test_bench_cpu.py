@@ -187,3 +187,54 @@ def test_empty_shard_is_rejected():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--roots-per-gpu", "0", "--dry-run"],
                        capture_output=True, text=True, timeout=120, env=_bench_env(), cwd=ROOT)
     assert r.returncode != 0 and "non-empty shard" in (r.stderr + r.stdout)
+
+
+def test_launch_stats_and_abba_summary():
+    """the line's kernel time is the median of the timed launches (one drifted launch cannot move frac);
+    the caller-bounds leg is timed A B B A against plain launches of the same window"""
+    import bench
+
+    st = bench.launch_stats([6.2, 6.21, 6.4, 6.19, 6.2])
+    assert st["n"] == 5 and st["min"] == 6.19 and st["max"] == 6.4 and st["median"] == 6.2
+    assert abs(st["mean"] - 6.24) < 1e-12
+    order = bench.abba_order(4)
+    assert order == [0, 1, 1, 0] * 4 and order.count(0) == order.count(1) == 8
+    # each leg follows each leg equally often: the predecessor mix is the same for A and B
+    follows = {(a, b): 0 for a in (0, 1) for b in (0, 1)}
+    for prev, cur in zip(order, order[1:]):
+        follows[(prev, cur)] += 1
+    assert follows[(0, 1)] == follows[(1, 0)]
+    ab = bench.ab_summary([6.4, 6.2, 6.2, 6.3], [6.2, 6.2, 6.1, 6.3])
+    assert ab["a"]["median"] == 6.25 and ab["b"]["median"] == 6.2
+    assert abs(ab["ratio_median"] - 6.2 / 6.25) < 1e-12
+
+
+def test_distinct_devices():
+    """a multi-GPU record proves N physical devices by UUID (or PCI location) per host, not by world size"""
+    import bench
+
+    same = [{"host": "h", "uuid": "GPU-1", "device_index": 0}] * 2
+    assert bench.distinct_devices(same) == 1
+    eight = [{"host": "h", "uuid": f"GPU-{k}", "device_index": k} for k in range(8)]
+    assert bench.distinct_devices(eight) == 8
+    pci = [{"host": "h", "pci_bus_id": str(b), "pci_device_id": "0", "pci_domain_id": "0"} for b in (3, 3, 4)]
+    assert bench.distinct_devices(pci) == 2
+    assert bench.distinct_devices([{"host": "a", "device_index": 0}, {"host": "b", "device_index": 0}]) == 2
+
+
+def test_gpus_8_driver_form_dry_run():
+    """the exact N = 8 driver form (bench.py --gpus 8, self-launched) rehearsed on gloo without a GPU:
+    8 ranks, every rank's LOCAL_RANK distinct, 8,192 roots each (configs[2] over 8 GPUs)"""
+    import subprocess
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--dist-backend", "gloo",
+                        "--dry-run"], capture_output=True, text=True, timeout=600, env=_bench_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 8 and rec["dist"]["world_size"] == 8
+    assert sorted(rec["dist"]["ranks"]) == list(range(8))
+    assert rec["dist"]["roots_per_rank"] == [8192] * 8
+    assert sorted(d["local_rank"] for d in rec["dist"]["devices"]) == list(range(8))
+    assert [d["rank"] for d in rec["dist"]["devices"]] == list(range(8))

@@ -600,31 +600,62 @@ def test_search_configs4_whole_batch_equals_oracle(mzh):
         assert d is None, f"{t} ({kern}): root Q / MinMaxStats differ in 256-root block {d[0]} of the shard"
 
 
+_LOCKSTEP_REF = {}
+
+
+def _lockstep_ref(oracle, B, S, n, replay):
+    """the oracle's per-simulation selection depths for the lockstep test's inputs (computed once)"""
+    key = (B, S, n, replay)
+    if key not in _LOCKSTEP_REF:
+        flat, in_dim, sup = _weights(oracle, f"weights_N{n}_s0")
+        obs, noise, tie, u = _random_search_inputs(B, n, 4321)
+        g = np.random.default_rng(5)
+        rp = dict(root_pi=g.dirichlet(np.full(6, 20.0), size=B).astype(np.float32),
+                  pi=g.dirichlet(np.full(6, 20.0), size=(B, S)).astype(np.float32),
+                  rwd=g.normal(0, 0.05, (B, S)).astype(np.float32), value=g.normal(0, 0.5, (B, S)).astype(np.float32))
+        if replay:
+            ref = oracle.search(n, S, obs, replay=rp, noise=noise, tie_idx=tie, action_u=u, temperature=1.0, depths=True)
+        else:
+            ref = oracle.search(n, S, obs, flat=flat, support=sup, noise=noise, tie_idx=tie, action_u=u,
+                                temperature=1.0, depths=True)
+        _LOCKSTEP_REF[key] = (flat, sup, obs, noise, tie, u, rp, ref)
+    return _LOCKSTEP_REF[key]
+
+
+@pytest.mark.parametrize("replay", [False, True])
 @pytest.mark.parametrize("kernel,tile", [("coop", 16), ("coop", 32), ("occ2", None), ("wave", None), ("wave16", None)])
-def test_search_lockstep_levels(mzh, oracle, kernel, tile):
+def test_search_lockstep_levels(mzh, oracle, kernel, tile, replay):
     """mzh_search_args.lockstep_levels (the select/backup latency model's input, bench.tree_latency_model):
-    per lockstep group the sum over simulations of its deepest selection below the root, so
-    max_r (sel_steps_r - S) <= levels_g <= sum_r (sel_steps_r - S) over the group's roots; asking for
-    it changes no other output (fused and replay searches)"""
+    per lockstep group (a workgroup of the cooperative kernels, a wave of the wave kernels) the sum over
+    simulations of its deepest selection below the root -- equal, group by group, to that sum over the
+    oracle's per-simulation selection depths, in the fused search and in the replay instantiation (the one
+    bench.py counts on); asking for it changes no other output"""
     from muzero_hanoi_amd import _lib
 
-    B, S, n = 2000, 30, 4
-    flat, in_dim, sup = _weights(oracle, f"weights_N{n}_s0")
-    obs, noise, tie, u = _random_search_inputs(B, n, 4321)
+    if replay and kernel == "occ2":
+        pytest.skip("the two-workgroups-per-CU kernel has no replay instantiation")
+    B, S, n = 600, 30, 4
+    flat, sup, obs, noise, tie, u, rp, ref = _lockstep_ref(oracle, B, S, n, replay)
     eng = _engine(mzh, n, S, B, sup, flat)
     tt = lambda a: torch.tensor(np.asarray(a), device=DEV)
-    kw = dict(obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0, kernel=kernel, tile=tile)
+    kw = dict(tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0, kernel=kernel, tile=tile)
+    if replay:
+        kw["replay"] = dict(root_pi=tt(rp["root_pi"]), pi=tt(rp["pi"]), reward=tt(rp["rwd"]), value=tt(rp["value"]))
+    else:
+        kw["obs"] = tt(obs)
     base = eng.search(S, **kw)
     lo = eng.search(S, out=eng.alloc_search_outputs(B, S, lockstep=True), **kw)
     pl = lo["_plan"]
     for k in ("visits", "root_q", "pi", "action", "sel_steps", "minmax"):
         assert torch.equal(base[k], lo[k]), k
+    assert np.array_equal(lo["sel_steps"].cpu().numpy(), ref["sel_steps"])
     g = pl["roots_per_wave"] if pl["wave"] else pl["roots_per_workgroup"]
     ng = -(-B // g)
     lv = lo["lockstep_levels"].cpu().numpy()
     assert (lv[ng:] == 0).all()
-    below = lo["sel_steps"].cpu().numpy().astype(np.int64) - S  # each simulation's levels below the root
-    for grp in range(ng):
-        d = below[grp * g:(grp + 1) * g]
-        assert d.max() <= lv[grp] <= d.sum(), (grp, lv[grp], d.max(), d.sum())
-    assert pl == _lib.search_plan(sup, B, S, mzh.search_flags(kernel, tile))
+    below = np.concatenate([ref["depths"] - 1, np.zeros((ng * g - B, S), np.int32)])
+    want = below.reshape(ng, g, S).max(1).sum(1)
+    bad = np.flatnonzero(lv[:ng] != want)
+    assert bad.size == 0, f"group {bad[0]}: kernel {lv[bad[0]]} levels, oracle {want[bad[0]]} ({bad.size} groups differ)"
+    if not replay:
+        assert pl == _lib.search_plan(sup, B, S, mzh.search_flags(kernel, tile))

@@ -78,7 +78,8 @@ def summarise(root, tag, want=None):
             d["mfma_busy_frac"] = d["SQ_INSTS_MFMA"] * 32 / (cyc * 1024)
             if "SQ_ACTIVE_INST_ANY" in d:
                 # the issue ceiling: cycles some wave of a SIMD issued (SQ_ACTIVE_INST_ANY counts quad-cycles per
-                # wave, summed over waves) over the SIMDs' cycles
+                # wave, summed over waves) over the SIMDs' cycles -- exact at one wave per SIMD, an upper bound
+                # with two (overlapping issue of the pair is counted twice; bench.py labels it so)
                 d["issue_frac"] = d["SQ_ACTIVE_INST_ANY"] * 4 / (cyc * 1024)
         if "SQ_WAIT_ANY" in d and "SQ_WAVE_CYCLES" in d:
             d["waitcnt_frac"] = d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"]  # wave cycles parked in s_waitcnt
