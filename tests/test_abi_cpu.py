@@ -113,6 +113,13 @@ def test_search_plan_query_names_the_instantiations(lib):
     assert (pl["wave"], pl["roots_per_workgroup"], pl["workgroups"], pl["threads_per_workgroup"]) == (0, 32, 256, 256)
     pl = lib.search_plan(33, 65536, 50)
     assert (pl["wave"], pl["roots_per_wave"], pl["workgroups"]) == (1, 32, 512)
+    # the forced two-workgroups-per-CU kernel: served where its LDS fits twice per CU, an error where it
+    # does not (no silent fallback), and replay searches name the cooperative replay kernel they run
+    occ2 = engine.search_flags("occ2")
+    assert P(8192, flags=occ2) == "mzh_search_occ2_kernel<true, false>"
+    with pytest.raises(RuntimeError, match="MZH_FLAG_COOP_OCC2"):
+        P(8192, 200, flags=occ2)
+    assert P(8192, 200, flags=occ2, replay=True).startswith("mzh_search_kernel<")
 
 
 def test_build_id_names_the_checked_out_sources(lib, tmp_path, monkeypatch):

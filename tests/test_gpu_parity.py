@@ -185,6 +185,17 @@ KERNELS = ["coop", "wave", "wave16"]
 KERNELS_MLP = KERNELS + ["occ2"]
 
 
+def _occ2_fits(support, S):
+    """whether the two-workgroups-per-CU kernel can serve an S-simulation search (its LDS twice per CU)"""
+    from muzero_hanoi_amd import _lib, engine
+
+    try:
+        _lib.search_plan(support, 64, S, engine.search_flags("occ2"))
+        return True
+    except RuntimeError:
+        return False
+
+
 @pytest.mark.parametrize("kernel", KERNELS_MLP)
 def test_search_confident_heads_vs_oracle(mzh, oracle, kernel):
     """the fused searches with confident heads (softmax IEEE fallback inside the search kernels'
@@ -304,8 +315,14 @@ def test_search_mlp_end_to_end_vs_oracle(mzh, oracle, case, kernel):
     B = g["obs"].shape[0]
     eng = _engine(mzh, n, S, B, sup, flat)
     tt = lambda a: None if a is None else torch.tensor(np.asarray(a), device=DEV)
-    o = eng.search(S, obs=tt(g["obs"].astype(np.float32)), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u),
-                   temperature=T, deterministic=det, discount=float(g["discount"]), kernel=kernel)
+    kw = dict(obs=tt(g["obs"].astype(np.float32)), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=T,
+              deterministic=det, discount=float(g["discount"]), kernel=kernel)
+    if kernel == "occ2" and not _occ2_fits(sup, S):
+        # a forced two-workgroups-per-CU search it cannot serve is an error, never a silent fallback (mzh.h)
+        with pytest.raises(RuntimeError, match="MZH_FLAG_COOP_OCC2"):
+            eng.search(S, **kw)
+        return
+    o = eng.search(S, **kw)
     o = {k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")}
     ref = oracle.search(n, S, g["obs"], flat=flat, support=sup, noise=noise, tie_idx=tie, action_u=u,
                         temperature=T, deterministic=det, discount=float(g["discount"]))
