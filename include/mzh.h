@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MZH_ABI_VERSION 4
+#define MZH_ABI_VERSION 5
 
 #define MZH_OK 0
 #define MZH_ERR_ARG (-1)         /* bad argument / shape (ValueError in Python)              */
@@ -52,6 +52,10 @@ extern "C" {
                                   CU fails with MZH_ERR_CAPACITY; a replay (tree-only) search, which has no
                                   occ2 instantiation, runs the cooperative replay kernel instead (the plan
                                   names it) */
+#define MZH_FLAG_KERNEL_ONE 128u /* force the latency kernel (mzh_search_one_kernel: one root per workgroup,
+                                    the network stationary on the CU; default for MLP searches of B <= 1024
+                                    roots whose LDS fits).  An error for replay searches, with another kernel
+                                    flag, or where its LDS does not fit */
 
 typedef struct mzh_engine mzh_engine;
 typedef void* mzh_stream; /* hipStream_t */

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "libmzh.so")
 LIB_PATH = os.environ.get("MZH_LIB") or DEFAULT_LIB  # MZH_LIB: diagnostic builds
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MZH_OK = 0
 MZH_ERR_ARG = -1
 MZH_ERR_HIP = -2
@@ -28,6 +28,7 @@ MZH_FLAG_KERNEL_WAVE16 = 8  # wave-independent kernel, 16 roots per wave
 MZH_FLAG_COOP_TILE16 = 16  # cooperative kernel, 16 roots per workgroup
 MZH_FLAG_COOP_TILE32 = 32  # cooperative kernel, 32 roots per workgroup
 MZH_FLAG_COOP_OCC2 = 64  # cooperative kernel, 16-root tiles, two workgroups per CU (mzh_search_occ2_kernel)
+MZH_FLAG_KERNEL_ONE = 128  # latency kernel: one root per workgroup, the network stationary on the CU (mzh_one.hip)
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32

@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 REPO = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libmzh.so")
 OBJ = os.path.join(HERE, "_obj")
-SOURCES = ["mzh_api.hip", "mzh_search.hip", "mzh_wave.hip", "mzh_env.hip", "mzh_train.hip"]
+SOURCES = ["mzh_api.hip", "mzh_search.hip", "mzh_wave.hip", "mzh_one.hip", "mzh_env.hip", "mzh_train.hip"]
 # host-only sources, compiled by g++ like the NumPy C code they restate (no -march: no FMA; see
 # csrc/mzh_rng.cpp)
 HOST_SOURCES = ["mzh_rng.cpp"]
@@ -29,7 +29,11 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=
 # MFMA accumulators in arch VGPRs instead of the heuristic's AGPRs, so no epilogue element needs a
 # v_accvgpr_read (8,192 roots -1.7%, 4,096 -2.0%; the wave kernels, built without it, measured neutral;
 # profiles/r05_vgpr_form_ab.json).  Register allocation only: the same instructions, bit-identical results.
-SOURCE_FLAGS = {"mzh_search.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+# mzh_one.hip (the latency kernel, 134 weight registers per lane at two waves per SIMD): no SLP vectorisation --
+# it packs the interleaved policy / value chains into v_pk_fma_f32, which needs each weight pair in adjacent
+# registers and copies the rows it shares with the other chains (231 spilled VGPRs with it, none in the loop
+# without it)
+SOURCE_FLAGS = {"mzh_search.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"], "mzh_one.hip": ["-fno-slp-vectorize"]}
 
 
 BUILD_ID_MARKER = b"MZH_BUILD_ID:"

@@ -58,6 +58,7 @@ struct mzh_engine {
   bool loaded = false;
   MzhNet net{};
   MzhWNet wnet{};
+  MzhOneNet onet{};
   unsigned char* tree = nullptr;
   float* htree = nullptr;
   uint16_t* pathx = nullptr;
@@ -261,6 +262,92 @@ static PackedW pack_wmlp(std::vector<float>& buf, const float* W1, const float* 
   return P;
 }
 
+// ---- latency-path packing (MzhOneNet, mzh_internal.h): float offsets of its arrays in the blob ----
+struct PackedOne {
+  size_t l1 = 0, b1 = 0, rep0 = 0, rep0b = 0, rep2 = 0, rep2b = 0, l2 = 0;
+};
+static PackedOne pack_one(std::vector<float>& buf, int in, int sup, const float* rep0w, const float* rep0b,
+                          const float* rep2w, const float* rep2b, const float* dyn0w, const float* dyn0b,
+                          const float* dyn2w, const float* dyn2b, const float* rwd0w, const float* rwd0b,
+                          const float* rwd2w, const float* rwd2b, const float* pol0w, const float* pol0b,
+                          const float* pol2w, const float* pol2b, const float* val0w, const float* val0b,
+                          const float* val2w, const float* val2b) {
+  const int H = MZH_LATENT, F = MZH_HIDDEN, A = MZH_ACTIONS;
+  auto align4 = [&]() { while (buf.size() % 4) buf.push_back(0.0f); };
+  PackedOne o;
+  // l1 [66 k4][256 units] float4
+  align4();
+  o.l1 = buf.size();
+  buf.resize(buf.size() + (size_t)66 * F * 4, 0.0f);
+  for (int k4 = 0; k4 < 66; ++k4)
+    for (int u = 0; u < F; ++u)
+      for (int i = 0; i < 4; ++i) {
+        float v = 0.0f;
+        if (k4 < 16) v = dyn0w[(size_t)u * (H + A) + 4 * k4 + i];
+        else if (k4 < 32) v = rwd0w[(size_t)u * H + 4 * (k4 - 16) + i];
+        else if (k4 < 48) v = pol0w[(size_t)u * H + 4 * (k4 - 32) + i];
+        else if (k4 < 64) v = val0w[(size_t)u * H + 4 * (k4 - 48) + i];
+        else if (4 * (k4 - 64) + i < A) v = dyn0w[(size_t)u * (H + A) + H + 4 * (k4 - 64) + i];
+        buf[o.l1 + ((size_t)k4 * F + u) * 4 + i] = v;
+      }
+  o.b1 = buf.size();
+  buf.resize(buf.size() + (size_t)F * 4);
+  for (int u = 0; u < F; ++u) {
+    buf[o.b1 + 4 * u] = dyn0b[u];
+    buf[o.b1 + 4 * u + 1] = rwd0b[u];
+    buf[o.b1 + 4 * u + 2] = pol0b[u];
+    buf[o.b1 + 4 * u + 3] = val0b[u];
+  }
+  // representation_net.0 k-major [in][256], its bias; representation_net.2 [64 k4][64] float4, its bias
+  o.rep0 = buf.size();
+  buf.resize(buf.size() + (size_t)in * F);
+  for (int k = 0; k < in; ++k)
+    for (int u = 0; u < F; ++u) buf[o.rep0 + (size_t)k * F + u] = rep0w[(size_t)u * in + k];
+  o.rep0b = buf.size();
+  buf.insert(buf.end(), rep0b, rep0b + F);
+  align4();
+  o.rep2 = buf.size();
+  buf.resize(buf.size() + (size_t)64 * 64 * 4);
+  for (int k4 = 0; k4 < 64; ++k4)
+    for (int j = 0; j < 64; ++j)
+      for (int i = 0; i < 4; ++i) buf[o.rep2 + ((size_t)k4 * 64 + j) * 4 + i] = rep2w[(size_t)j * F + 4 * k4 + i];
+  o.rep2b = buf.size();
+  buf.insert(buf.end(), rep2b, rep2b + H);
+  // the LDS image
+  align4();
+  o.l2 = buf.size();
+  buf.resize(buf.size() + (size_t)MZH_ONE_L2F4 * 4, 0.0f);
+  float* L = buf.data() + o.l2;
+  const int nb = sup < 32 ? sup : 32;  // bins of each head in the A2 rows
+  for (int k4 = 0; k4 < 64; ++k4)
+    for (int j = 0; j < 64; ++j)
+      for (int i = 0; i < 4; ++i) {
+        const int k = 4 * k4 + i;
+        L[((size_t)MZH_ONE_D2 + k4 * 64 + j) * 4 + i] = dyn2w[(size_t)j * F + k];
+        const int row = j & 31;
+        const float* W2 = j < 32 ? rwd2w : val2w;
+        L[((size_t)MZH_ONE_A2 + k4 * 64 + j) * 4 + i] = row < nb ? W2[(size_t)row * F + k] : 0.0f;
+        if (j < 8) L[((size_t)MZH_ONE_P2 + k4 * 8 + j) * 4 + i] = j < A ? pol2w[(size_t)j * F + k] : 0.0f;
+      }
+  if (sup == 33)
+    for (int i = 0; i < 64; ++i)
+      for (int ln = 0; ln < 8; ++ln) {
+        const float* W2 = ln < 4 ? rwd2w : val2w;
+        L[(size_t)MZH_ONE_C32 * 4 + i * 8 + ln] = W2[(size_t)32 * F + (ln & 3) + 4 * i];
+      }
+  float* B2 = L + (size_t)MZH_ONE_B2 * 4;
+  for (int j = 0; j < 64; ++j) {
+    B2[j] = dyn2b[j];
+    B2[64 + j] = (j & 31) < nb ? (j < 32 ? rwd2b : val2b)[j & 31] : 0.0f;
+  }
+  for (int j = 0; j < A; ++j) B2[128 + j] = pol2b[j];
+  if (sup == 33) {
+    B2[136] = rwd2b[32];
+    B2[137] = val2b[32];
+  }
+  return o;
+}
+
 extern "C" int mzh_load_weights(mzh_engine* eng, const float* flat, size_t n_floats) {
   if (!eng || !flat) return fail(MZH_ERR_ARG, "engine or weights NULL");
   const size_t want = canonical_size(eng->in_dim, eng->support);
@@ -310,6 +397,9 @@ extern "C" int mzh_load_weights(mzh_engine* eng, const float* flat, size_t n_flo
   buf.resize(buf.size() + (size_t)A * F, 0.0f);
   for (int a = 0; a < A; ++a)
     for (int j = 0; j < F; ++j) buf[wohoff + (size_t)a * F + j] = dyn0w[(size_t)wperm_u(j >> 4, j & 15) * (H + A) + H + a];
+  // latency-path layout
+  const PackedOne PO = pack_one(buf, in, sup, rep0w, rep0b, rep2w, rep2b, dyn0w, dyn0b, dyn2w, dyn2b, rwd0w, rwd0b,
+                                rwd2w, rwd2b, pol0w, pol0b, pol2w, pol2b, val0w, val0b, val2w, val2b);
 
   DeviceGuard g(eng->device);
   if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
@@ -370,6 +460,14 @@ extern "C" int mzh_load_weights(mzh_engine* eng, const float* flat, size_t n_flo
   w.oh = base + wohoff;
   w.support = sup;
   w.in_dim = in;
+  MzhOneNet& o = eng->onet;
+  o.l1 = reinterpret_cast<const float4*>(base + PO.l1);
+  o.b1 = reinterpret_cast<const float4*>(base + PO.b1);
+  o.rep0 = base + PO.rep0;
+  o.rep0b = base + PO.rep0b;
+  o.rep2 = reinterpret_cast<const float4*>(base + PO.rep2);
+  o.rep2b = base + PO.rep2b;
+  o.l2 = reinterpret_cast<const float4*>(base + PO.l2);
   eng->loaded = true;
   return MZH_OK;
 }
@@ -483,8 +581,39 @@ static KernelChoice choose_kernel(int B, uint32_t flags) {
   return {false, 0};
 }
 
+// the latency path (mzh_one.hip): MLP searches of up to kOneMaxRoots roots take one root per workgroup
+// (persistent over the roots beyond the 256 workgroups of one round) while its LDS fits; a forced kernel
+// flag (or MZH_KERNEL) decides otherwise.  MZH_FLAG_KERNEL_ONE forces it (an error where it cannot run).
+static const int kOneMaxRoots = 1024, kOneGrid = 256;
+static bool one_forced_env() {
+  static const bool f = [] {
+    const char* v = getenv("MZH_KERNEL");
+    return v && strcmp(v, "one") == 0;
+  }();
+  return f;
+}
+
 // every template argument of the launch (MzhSearchPlan); returns a status (capacity errors)
 static int make_plan(int B, int S, uint32_t flags, bool replay, int support, bool has_minmax, MzhSearchPlan* pl) {
+  const uint32_t forced = flags & (MZH_FLAG_KERNEL_COOP | MZH_FLAG_KERNEL_WAVE | MZH_FLAG_KERNEL_WAVE16 | MZH_FLAG_COOP_OCC2 |
+                                   MZH_FLAG_COOP_TILE16 | MZH_FLAG_COOP_TILE32);
+  const bool one_fits = mzh_one_smem_bytes(S) <= kMaxLds;
+  if (flags & MZH_FLAG_KERNEL_ONE) {
+    if (replay) return fail(MZH_ERR_ARG, "MZH_FLAG_KERNEL_ONE: the latency kernel has no replay (tree-only) form");
+    if (forced) return fail(MZH_ERR_ARG, "MZH_FLAG_KERNEL_ONE combined with another kernel flag");
+    if (!one_fits) return fail(MZH_ERR_CAPACITY, "MZH_FLAG_KERNEL_ONE: n_sims=%d needs %zu B of LDS", S, mzh_one_smem_bytes(S));
+  }
+  const bool env_kernel = getenv("MZH_KERNEL") != nullptr;
+  if (!replay && one_fits &&
+      ((flags & MZH_FLAG_KERNEL_ONE) || one_forced_env() || (!forced && !env_kernel && B <= kOneMaxRoots))) {
+    MzhSearchPlan q{};
+    q.one = 1;
+    q.sup33 = support == 33;
+    q.mmin = has_minmax ? 1 : 0;
+    q.grid = B < kOneGrid ? B : kOneGrid;
+    *pl = q;
+    return MZH_OK;
+  }
   const KernelChoice kc = choose_kernel(B, flags);
   MzhSearchPlan q{};
   q.wave = kc.wave ? 1 : 0;
@@ -527,6 +656,15 @@ static void plan_info(const MzhSearchPlan& q, int B, int S, mzh_search_plan* out
   memset(out, 0, sizeof(*out));
   const char* tf[2] = {"false", "true"};
   out->wave = q.wave;
+  if (q.one) {
+    out->roots_per_wave = 1;
+    out->threads_per_workgroup = 512;
+    out->roots_per_workgroup = 1;
+    out->smem_bytes = (int64_t)mzh_one_smem_bytes(S);
+    snprintf(out->kernel, sizeof(out->kernel), "mzh_search_one_kernel<%s, %s>", tf[q.sup33], tf[q.mmin]);
+    out->workgroups = q.grid;
+    return;
+  }
   if (q.wave) {
     out->roots_per_wave = 16 * q.nt;
     out->threads_per_workgroup = 256;
@@ -602,8 +740,9 @@ static int search_common(mzh_engine* eng, const mzh_search_args* a, mzh_stream s
   p.visits = a->visits; p.root_q = a->root_q; p.minmax_out = a->minmax_out; p.extra_ties = a->extra_ties;
   p.action = a->action; p.pi = a->pi; p.latent = a->latent; p.latent_len = a->latent_len; p.sel_steps = a->sel_steps; p.lockstep_levels = a->lockstep_levels;
   p.pow_table = a->pow_table;
-  hipError_t e = pl.wave ? mzh_launch_wave_search(pl, eng->wnet, p, (hipStream_t)stream)
-                         : mzh_launch_search(pl, eng->net, p, (hipStream_t)stream);
+  hipError_t e = pl.one ? mzh_launch_one(pl, eng->net, eng->onet, p, (hipStream_t)stream)
+                 : pl.wave ? mzh_launch_wave_search(pl, eng->wnet, p, (hipStream_t)stream)
+                           : mzh_launch_search(pl, eng->net, p, (hipStream_t)stream);
   return e == hipSuccess ? MZH_OK : hip_fail(e, "search launch");
 }
 

@@ -121,6 +121,36 @@ struct MzhWNet {
   int support, in_dim;
 };
 
+// ------------------------------------------------------------------------------------------
+// Latency-path network layout (mzh_one.hip: one root per workgroup, weights stationary on the CU).
+// The hidden layers' rows live in registers for the whole launch: thread t < 256 holds unit t of
+// dynamic_net.0 (64 latent + 6 one-hot columns) and rwd_net.0, thread 256 + t unit t of policy_net.0 and
+// value_net.0.  The K = 256 output layers live in LDS, copied verbatim from `l2` (k-major: one
+// ds_read_b128 gives a lane the 4 k-steps of its output row, 1 KiB contiguous per wave).
+//   l1 [66 k4][256 units] float4: k4 0-15 dynamic_net.0 latent columns, 16-31 rwd_net.0, 32-47 policy_net.0,
+//      48-63 value_net.0, 64-65 dynamic_net.0 one-hot columns 64..69 (+ 2 zero)
+//   b1 [256] float4 {dynamic_net.0, rwd_net.0, policy_net.0, value_net.0} bias of the unit
+//   rep0 [in_dim][256] representation_net.0 (k-major), rep2 [64 k4][64] float4 representation_net.2
+//   l2: the LDS image, MZH_ONE_* offsets in float4 units
+// ------------------------------------------------------------------------------------------
+#define MZH_ONE_D2 0                        // dynamic_net.2 [64 k4][64 lanes]
+#define MZH_ONE_A2 (64 * 64)                // rwd_net.2 bins 0-31 (lanes 0-31) | value_net.2 bins 0-31 (lanes 32-63)
+#define MZH_ONE_P2 (2 * 64 * 64)            // policy_net.2 [64 k4][8 lanes] (6 rows + 2 zero)
+#define MZH_ONE_C32 (MZH_ONE_P2 + 64 * 8)   // bin 32 chains [64 i][8 lanes] floats: lane g < 4 the reward head's
+                                            // chain g (k = g + 4i), lane 4 + g the value head's (128 float4)
+#define MZH_ONE_B2 (MZH_ONE_C32 + 128)      // biases (floats): [0,64) dynamic_net.2, [64,128) the A2 rows,
+                                            // [128,136) policy_net.2, 136 / 137 bin 32 of reward / value
+#define MZH_ONE_L2F4 (MZH_ONE_B2 + 36)      // float4s of the LDS image
+struct MzhOneNet {
+  const float4* l1;
+  const float4* b1;
+  const float* rep0;
+  const float* rep0b;
+  const float4* rep2;
+  const float* rep2b;
+  const float4* l2;
+};
+
 // Every template argument of one search launch, decided once on the host (mzh_api.hip make_plan) and
 // used both to launch and to report the launched instantiation (mzh_search_plan_query)
 struct MzhSearchPlan {
@@ -130,10 +160,15 @@ struct MzhSearchPlan {
   int replay;  // tree-only instantiation (recorded network outputs)
   int ohl;     // cooperative: the dynamics one-hot columns in LDS
   int sup33;   // 33-bin value / reward support (cooperative replay: always 1, one instantiation)
-  int mmin;    // cooperative: caller-given MinMaxStats bounds (subnormal max - min check)
+  int mmin;    // cooperative / one: caller-given MinMaxStats bounds (subnormal max - min check)
   int occ2;    // cooperative: mzh_search_occ2_kernel<sup33, mmin> (16-root tile, two workgroups per CU)
+  int one;     // latency path: mzh_search_one_kernel<sup33, mmin> (one root per workgroup)
+  int grid;    // one: workgroups (each loops over roots b, b + grid, ...)
 };
 
+size_t mzh_one_smem_bytes(int S);
+hipError_t mzh_launch_one(const MzhSearchPlan& pl, const MzhNet& net, const MzhOneNet& on, const MzhSearchParams& p,
+                          hipStream_t stream);
 size_t mzh_wave_smem_bytes(int S, int nt);
 hipError_t mzh_launch_wave_search(const MzhSearchPlan& pl, const MzhWNet& net, const MzhSearchParams& p, hipStream_t stream);
 size_t mzh_search_smem_bytes(int R, int S, bool ohl, bool occ2 = false);

@@ -147,7 +147,8 @@ class Engine:
                kernel=None, tile=None):
         """Batched search. Tensors must already be on the device (bench: inputs resident in HBM).
         replay = dict(root_pi, pi, reward, value) -> tree-only mode (mzh_search_replay).
-        kernel = None (automatic by batch size) | "coop" | "wave" | "wave16" (all give identical results);
+        kernel = None (automatic by batch size) | "coop" | "occ2" | "wave" | "wave16" | "one" (all give identical
+        results; "one" = the latency kernel, MLP searches only);
         tile = None | 16 | 32: the cooperative kernel's roots per workgroup (default by batch size)."""
         B = int(tie_idx.shape[0])
         if out is None:
@@ -202,12 +203,12 @@ class Engine:
 
 
 def search_flags(kernel=None, tile=None, np1_ucb=False):
-    """mzh_search_args.flags for a kernel choice (None | "coop" | "occ2" | "wave" | "wave16") and coop tile
-    ("occ2": the cooperative kernel's two-workgroups-per-CU 16-root form)"""
+    """mzh_search_args.flags for a kernel choice (None | "coop" | "occ2" | "wave" | "wave16" | "one") and coop
+    tile ("occ2": the cooperative kernel's two-workgroups-per-CU 16-root form; "one": the latency kernel)"""
     f = _lib.MZH_FLAG_NP1_UCB if np1_ucb else 0
     f |= {None: 0, "auto": 0, "coop": _lib.MZH_FLAG_KERNEL_COOP, "wave": _lib.MZH_FLAG_KERNEL_WAVE,
           "wave16": _lib.MZH_FLAG_KERNEL_WAVE16,
-          "occ2": _lib.MZH_FLAG_KERNEL_COOP | _lib.MZH_FLAG_COOP_OCC2}[kernel]
+          "occ2": _lib.MZH_FLAG_KERNEL_COOP | _lib.MZH_FLAG_COOP_OCC2, "one": _lib.MZH_FLAG_KERNEL_ONE}[kernel]
     return f | {None: 0, 16: _lib.MZH_FLAG_COOP_TILE16, 32: _lib.MZH_FLAG_COOP_TILE32}[tile]
 
 

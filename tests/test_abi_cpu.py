@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol(lib):
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(lib.SIGNATURES), "ctypes signature table out of sync with include/mzh.h"
-    assert L.mzh_abi_version() == lib.ABI_VERSION == 4
+    assert L.mzh_abi_version() == lib.ABI_VERSION == 5
 
 
 def _c_offsets(struct, fields, tmp_path):
@@ -88,7 +88,23 @@ def test_search_plan_query_names_the_instantiations(lib):
     assert P(8192) == "mzh_search_kernel<32, false, true, true, false>"
     assert P(4097) == "mzh_search_kernel<32, false, true, true, false>"
     assert P(4096) == "mzh_search_kernel<16, false, true, true, false>"
-    assert P(1) == "mzh_search_kernel<16, false, true, true, false>"
+    assert P(1025) == "mzh_search_kernel<16, false, true, true, false>"
+    # the latency kernel: MLP searches of <= 1,024 roots (one root per workgroup, up to 256 workgroups)
+    assert P(1024) == P(1) == "mzh_search_one_kernel<true, false>"
+    assert P(1, minmax_in=True) == "mzh_search_one_kernel<true, true>"
+    assert lib.search_plan(1, 1, 25)["kernel"] == "mzh_search_one_kernel<false, false>"
+    pl = lib.search_plan(33, 1000, 25)
+    assert (pl["workgroups"], pl["roots_per_workgroup"], pl["threads_per_workgroup"]) == (256, 1, 512)
+    assert lib.search_plan(33, 7, 25)["workgroups"] == 7
+    assert P(1, replay=True) == "mzh_search_kernel<16, true, false, true, false>"  # no replay form
+    assert P(1, 200) == "mzh_search_kernel<16, false, true, true, false>"  # its LDS does not fit: cooperative
+    assert P(1, flags=engine.search_flags("coop")) == "mzh_search_kernel<16, false, true, true, false>"
+    assert P(4096, flags=engine.search_flags("one")) == "mzh_search_one_kernel<true, false>"
+    for bad in (dict(S=200), dict(replay=True), dict(flags=engine.search_flags("one", tile=16))):
+        kw = dict(bad)
+        S = kw.pop("S", 50)
+        with pytest.raises((RuntimeError, ValueError), match="MZH_FLAG_KERNEL_ONE"):
+            P(1, S, flags=kw.pop("flags", engine.search_flags("one")), **kw)
     # caller MinMaxStats bounds (every run_mcts / self-play search): one-hot table still in LDS
     assert P(4096, minmax_in=True) == "mzh_search_kernel<16, false, true, true, true>"
     assert P(8192, minmax_in=True) == "mzh_search_kernel<32, false, true, true, true>"
@@ -102,6 +118,7 @@ def test_search_plan_query_names_the_instantiations(lib):
     assert P(8192, flags=engine.search_flags(tile=16)) == "mzh_search_kernel<16, false, true, true, false>"
     assert P(100, flags=engine.search_flags(tile=32)) == "mzh_search_kernel<32, false, true, true, false>"
     assert P(100, flags=engine.search_flags("wave")) == "mzh_wave_kernel<2, false, true>"
+    assert P(100, flags=engine.search_flags("occ2")) == "mzh_search_occ2_kernel<true, false>"
     assert P(70000, flags=engine.search_flags("coop")) == "mzh_search_kernel<32, false, true, true, false>"
     assert P(70000, flags=engine.search_flags("wave16")) == "mzh_wave_kernel<1, false, true>"
     # deep trees: the 32-root tile's LDS path budget gives way to 16 roots, then to a capacity error

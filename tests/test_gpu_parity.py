@@ -182,15 +182,17 @@ def test_softmax_fallback_confident_heads_vs_oracle(mzh, oracle):
 # ------------------------------------------------------------------------------------ search
 KERNELS = ["coop", "wave", "wave16"]
 # MLP searches: also the two-workgroups-per-CU cooperative form (replay searches have no such form)
-KERNELS_MLP = KERNELS + ["occ2"]
+# and the latency kernel (one root per workgroup, mzh_one.hip)
+KERNELS_MLP = KERNELS + ["occ2", "one"]
 
 
-def _occ2_fits(support, S):
-    """whether the two-workgroups-per-CU kernel can serve an S-simulation search (its LDS twice per CU)"""
+def _forced_fits(kernel, support, S):
+    """whether a forced kernel can serve an S-simulation search (the two-workgroups-per-CU kernel: its LDS twice
+    per CU; the latency kernel: its LDS tree and tables beside the output layers)"""
     from muzero_hanoi_amd import _lib, engine
 
     try:
-        _lib.search_plan(support, 64, S, engine.search_flags("occ2"))
+        _lib.search_plan(support, 64, S, engine.search_flags(kernel))
         return True
     except RuntimeError:
         return False
@@ -317,9 +319,9 @@ def test_search_mlp_end_to_end_vs_oracle(mzh, oracle, case, kernel):
     tt = lambda a: None if a is None else torch.tensor(np.asarray(a), device=DEV)
     kw = dict(obs=tt(g["obs"].astype(np.float32)), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=T,
               deterministic=det, discount=float(g["discount"]), kernel=kernel)
-    if kernel == "occ2" and not _occ2_fits(sup, S):
-        # a forced two-workgroups-per-CU search it cannot serve is an error, never a silent fallback (mzh.h)
-        with pytest.raises(RuntimeError, match="MZH_FLAG_COOP_OCC2"):
+    if kernel in ("occ2", "one") and not _forced_fits(kernel, sup, S):
+        # a forced kernel that cannot serve the search is an error, never a silent fallback (mzh.h)
+        with pytest.raises(RuntimeError, match="MZH_FLAG_COOP_OCC2" if kernel == "occ2" else "MZH_FLAG_KERNEL_ONE"):
             eng.search(S, **kw)
         return
     o = eng.search(S, **kw)
@@ -337,7 +339,7 @@ def test_search_mlp_end_to_end_vs_oracle(mzh, oracle, case, kernel):
 
 
 @pytest.mark.parametrize("kernel,tile", [("coop", None), ("coop", 16), ("coop", 32), ("wave", None), ("wave16", None),
-                                         ("occ2", None)])
+                                         ("occ2", None), ("one", None)])
 @pytest.mark.parametrize("B,S,n", [(40, 50, 4), (700, 25, 3), (9000, 8, 4), (300, 20, 7)])
 def test_search_batched_vs_oracle_random_roots(mzh, oracle, B, S, n, kernel, tile):
     """Ragged batches (not multiples of the 16/32-root tile), both tile sizes forced and by
@@ -534,7 +536,7 @@ def test_search_caller_bounds_instantiation(mzh, oracle, B, tile):
 FULL_BATCH = [("c1_4096", None), ("c3_16384", None), ("c2_65536", None), ("c4_shard0of8", None),
               ("c2_shard7of8", None), ("c2_shard7of8", "occ2"), ("c2_shard7of8", "coop"), ("c1_4096", "occ2"),
               ("c1_4096_s1", None), ("c1_4096_s2", None), ("c1_4096_s3", None), ("c1_4096_s4", None),
-              ("c1_4096_det", None), ("c1_4096_det", "wave16")]
+              ("c1_4096_det", None), ("c1_4096_det", "wave16"), ("c1_4096", "one"), ("c1_4096_det", "one")]
 
 
 def _first_diff(a, b):
@@ -567,8 +569,8 @@ def test_search_full_batch_equals_oracle(mzh, tag, kernel):
     o = eng.search(S, obs=tt(obs), tie_idx=tt(tie), noise=tt(noise), action_u=tt(u), temperature=1.0,
                    deterministic=gf.deterministic(tag), discount=0.8, eps=0.25, kernel=kernel)
     kern = o["_plan"]["kernel"]
-    if kernel == "occ2":
-        assert kern.startswith("mzh_search_occ2_kernel<"), kern
+    if kernel in ("occ2", "one"):
+        assert kern.startswith(f"mzh_search_{kernel}_kernel<"), kern
     o = {k: v.cpu().numpy() for k, v in o.items() if not k.startswith("_")}
     eng.close()
     for k, want in (("visits", z["visits"]), ("action", z["action"]), ("sel_steps", z["sel_steps"]),
@@ -640,7 +642,8 @@ def _lockstep_ref(oracle, B, S, n, replay):
 
 
 @pytest.mark.parametrize("replay", [False, True])
-@pytest.mark.parametrize("kernel,tile", [("coop", 16), ("coop", 32), ("occ2", None), ("wave", None), ("wave16", None)])
+@pytest.mark.parametrize("kernel,tile", [("coop", 16), ("coop", 32), ("occ2", None), ("wave", None), ("wave16", None),
+                                         ("one", None)])
 def test_search_lockstep_levels(mzh, oracle, kernel, tile, replay):
     """mzh_search_args.lockstep_levels (the select/backup latency model's input, bench.tree_latency_model):
     per lockstep group (a workgroup of the cooperative kernels, a wave of the wave kernels) the sum over
@@ -649,8 +652,8 @@ def test_search_lockstep_levels(mzh, oracle, kernel, tile, replay):
     bench.py counts on); asking for it changes no other output"""
     from muzero_hanoi_amd import _lib
 
-    if replay and kernel == "occ2":
-        pytest.skip("the two-workgroups-per-CU kernel has no replay instantiation")
+    if replay and kernel in ("occ2", "one"):
+        pytest.skip(f"the {kernel} kernel has no replay instantiation")
     B, S, n = 600, 30, 4
     flat, sup, obs, noise, tie, u, rp, ref = _lockstep_ref(oracle, B, S, n, replay)
     eng = _engine(mzh, n, S, B, sup, flat)
