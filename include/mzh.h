@@ -176,7 +176,8 @@ typedef struct mzh_search_args {
   const double* pow_table;
   /* [lockstep groups] (nullable; entries of groups without roots are left untouched): per group of roots
    * that advance through a simulation together -- a wave of the wave kernel (16 or 32 roots, index
-   * blockIdx * 4 + wave), a workgroup of the cooperative kernels -- the sum over simulations of the
+   * blockIdx * 4 + wave), a workgroup of the cooperative kernels, each root of the latency kernel (index =
+   * root; so B entries cover every plan) -- the sum over simulations of the
    * group's deepest selection below the root, i.e. the dependent tree-block loads the group waits for in
    * sequence (the select / backup latency model, bench.py roofline.tree.latency) */
   int32_t* lockstep_levels;

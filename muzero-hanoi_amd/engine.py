@@ -110,10 +110,10 @@ class Engine:
 
     # ---------------------------------------------------------------- search
     def alloc_search_outputs(self, B, n_sims, lockstep=False):
-        """lockstep=True adds lockstep_levels (zeroed, one entry per group of roots that advance together:
-        B // 16 + 1 covers every kernel's groups)"""
+        """lockstep=True adds lockstep_levels (zeroed, one entry per group of roots that advance together: at most
+        one per root -- the latency kernel's groups are single roots)"""
         d = self.device
-        extra = {"lockstep_levels": torch.zeros(B // 16 + 1, dtype=torch.int32, device=d)} if lockstep else {}
+        extra = {"lockstep_levels": torch.zeros(B + 1, dtype=torch.int32, device=d)} if lockstep else {}
         return dict(**extra,
             visits=torch.empty((B, ACTIONS), dtype=torch.int32, device=d),
             root_q=torch.empty(B, dtype=torch.float64, device=d),
