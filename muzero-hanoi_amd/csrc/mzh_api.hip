@@ -333,7 +333,7 @@ static PackedOne pack_one(std::vector<float>& buf, int in, int sup, const float*
     for (int i = 0; i < 64; ++i)
       for (int ln = 0; ln < 8; ++ln) {
         const float* W2 = ln < 4 ? rwd2w : val2w;
-        L[(size_t)MZH_ONE_C32 * 4 + i * 8 + ln] = W2[(size_t)32 * F + (ln & 3) + 4 * i];
+        L[(size_t)MZH_ONE_C32 * 4 + ln * 64 + i] = W2[(size_t)32 * F + (ln & 3) + 4 * i];
       }
   float* B2 = L + (size_t)MZH_ONE_B2 * 4;
   for (int j = 0; j < 64; ++j) {
@@ -597,17 +597,19 @@ static bool one_forced_env() {
 static int make_plan(int B, int S, uint32_t flags, bool replay, int support, bool has_minmax, MzhSearchPlan* pl) {
   const uint32_t forced = flags & (MZH_FLAG_KERNEL_COOP | MZH_FLAG_KERNEL_WAVE | MZH_FLAG_KERNEL_WAVE16 | MZH_FLAG_COOP_OCC2 |
                                    MZH_FLAG_COOP_TILE16 | MZH_FLAG_COOP_TILE32);
-  const bool one_fits = mzh_one_smem_bytes(S) <= kMaxLds;
+  const bool one_fits = mzh_one_smem_bytes(S, false) <= kMaxLds;
   if (flags & MZH_FLAG_KERNEL_ONE) {
     if (replay) return fail(MZH_ERR_ARG, "MZH_FLAG_KERNEL_ONE: the latency kernel has no replay (tree-only) form");
     if (forced) return fail(MZH_ERR_ARG, "MZH_FLAG_KERNEL_ONE combined with another kernel flag");
-    if (!one_fits) return fail(MZH_ERR_CAPACITY, "MZH_FLAG_KERNEL_ONE: n_sims=%d needs %zu B of LDS", S, mzh_one_smem_bytes(S));
+    if (!one_fits)
+      return fail(MZH_ERR_CAPACITY, "MZH_FLAG_KERNEL_ONE: n_sims=%d needs %zu B of LDS", S, mzh_one_smem_bytes(S, false));
   }
   const bool env_kernel = getenv("MZH_KERNEL") != nullptr;
   if (!replay && one_fits &&
       ((flags & MZH_FLAG_KERNEL_ONE) || one_forced_env() || (!forced && !env_kernel && B <= kOneMaxRoots))) {
     MzhSearchPlan q{};
     q.one = 1;
+    q.ohl = mzh_one_smem_bytes(S, true) <= kMaxLds;  // the latents in LDS where they fit
     q.sup33 = support == 33;
     q.mmin = has_minmax ? 1 : 0;
     q.grid = B < kOneGrid ? B : kOneGrid;
@@ -660,8 +662,8 @@ static void plan_info(const MzhSearchPlan& q, int B, int S, mzh_search_plan* out
     out->roots_per_wave = 1;
     out->threads_per_workgroup = 512;
     out->roots_per_workgroup = 1;
-    out->smem_bytes = (int64_t)mzh_one_smem_bytes(S);
-    snprintf(out->kernel, sizeof(out->kernel), "mzh_search_one_kernel<%s, %s>", tf[q.sup33], tf[q.mmin]);
+    out->smem_bytes = (int64_t)mzh_one_smem_bytes(S, q.ohl);
+    snprintf(out->kernel, sizeof(out->kernel), "mzh_search_one_kernel<%s, %s, %s>", tf[q.sup33], tf[q.mmin], tf[q.ohl]);
     out->workgroups = q.grid;
     return;
   }

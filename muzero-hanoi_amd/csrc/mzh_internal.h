@@ -136,7 +136,7 @@ struct MzhWNet {
 #define MZH_ONE_D2 0                        // dynamic_net.2 [64 k4][64 lanes]
 #define MZH_ONE_A2 (64 * 64)                // rwd_net.2 bins 0-31 (lanes 0-31) | value_net.2 bins 0-31 (lanes 32-63)
 #define MZH_ONE_P2 (2 * 64 * 64)            // policy_net.2 [64 k4][8 lanes] (6 rows + 2 zero)
-#define MZH_ONE_C32 (MZH_ONE_P2 + 64 * 8)   // bin 32 chains [64 i][8 lanes] floats: lane g < 4 the reward head's
+#define MZH_ONE_C32 (MZH_ONE_P2 + 64 * 8)   // bin 32 chains [8 lanes][64 i] floats: lane g < 4 the reward head's
                                             // chain g (k = g + 4i), lane 4 + g the value head's (128 float4)
 #define MZH_ONE_B2 (MZH_ONE_C32 + 128)      // biases (floats): [0,64) dynamic_net.2, [64,128) the A2 rows,
                                             // [128,136) policy_net.2, 136 / 137 bin 32 of reward / value
@@ -158,7 +158,7 @@ struct MzhSearchPlan {
   int nt;      // wave kernel: 16-root column tiles per wave
   int R;       // cooperative kernel: roots per workgroup
   int replay;  // tree-only instantiation (recorded network outputs)
-  int ohl;     // cooperative: the dynamics one-hot columns in LDS
+  int ohl;     // cooperative: the dynamics one-hot columns in LDS; one: the latents in LDS
   int sup33;   // 33-bin value / reward support (cooperative replay: always 1, one instantiation)
   int mmin;    // cooperative / one: caller-given MinMaxStats bounds (subnormal max - min check)
   int occ2;    // cooperative: mzh_search_occ2_kernel<sup33, mmin> (16-root tile, two workgroups per CU)
@@ -166,7 +166,7 @@ struct MzhSearchPlan {
   int grid;    // one: workgroups (each loops over roots b, b + grid, ...)
 };
 
-size_t mzh_one_smem_bytes(int S);
+size_t mzh_one_smem_bytes(int S, bool latl);
 hipError_t mzh_launch_one(const MzhSearchPlan& pl, const MzhNet& net, const MzhOneNet& on, const MzhSearchParams& p,
                           hipStream_t stream);
 size_t mzh_wave_smem_bytes(int S, int nt);

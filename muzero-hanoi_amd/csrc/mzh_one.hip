@@ -27,35 +27,139 @@
 namespace {
 constexpr int kThreads = 512;  // 8 waves: two per SIMD, 256 registers each
 
+// Activations in the "row layouts" the chains read (one_rows): a K = 256 vector as T[16][20] (element 16v + j at
+// T[j][v]: lane l finds x[16v + (l & 15)], v = 0..15, in four ds_read_b128; the stride of 20 floats puts the 16 rows'
+// reads in distinct banks), a K = 64 vector as T[16][4]; the bin-32 chains' copies Q[4][68] (unit g + 4i at Q[g][i]).
 struct MzhOneSmem {
-  float obs[64];    // root observation (zero-padded)
-  float xl[64];     // MLP input: the leaf's parent latent
-  float hidD[256];  // dynamics hidden (root: representation hidden)
-  float hraw[64];   // un-normalised latent (the reward head's input, networks.py:132-135)
-  float xh[64];     // normalised latent (the prediction input)
-  float hidR[256], hidP[256], hidV[256];
-  float lrwd[40], lval[40], lpol[16];  // logits (natural order; mzh_heads_row strides MZH_LDSUP / MZH_LDPOL)
-  float pi[8], value[1], reward[1];    // mzh_heads_row's STORE outputs (not used: STORE = false)
-  int act;                             // the leaf's action (one-hot column of the next dyn0)
+  float obs[64];                        // root observation (zero-padded)
+  float xlT[64];                        // MLP input: the leaf's parent latent (T64)
+  float hidDT[320];                     // dynamics (root: representation) hidden (T256)
+  float hrawT[64];                      // un-normalised latent, the reward head's input (networks.py:132-135) (T64)
+  float xhT[64];                        // normalised latent, the prediction input (T64)
+  float hidRT[320], hidPT[320], hidVT[320];  // reward / policy / value hidden (T256)
+  float hidRQ[272], hidVQ[272];         // reward / value hidden for bin 32's chains (Q)
+  float lrwd[40], lval[40], lpol[16];   // logits (natural order)
+  int act;                              // the leaf's action (one-hot column of the next dyn0)
   int pad[3];
-  MzhRootBlk root;                     // the root's 6 children (slots 6, 7 padding)
+  MzhRootBlk root;                      // the root's 6 children (slots 6, 7 padding)
+  MzhRootReg rsv;                       // the root's search state between tree phases (not live in registers
+                                        // across the MLP: every register there holds weights or chain operands)
 };
+__device__ __forceinline__ int one_t256(int n) { return (n & 15) * 20 + (n >> 4); }
+__device__ __forceinline__ int one_t64(int j) { return (j & 15) * 4 + (j >> 4); }
+__device__ __forceinline__ int one_q(int n) { return (n & 3) * 68 + (n >> 2); }
 
-// LDS: the activations first (every access a small immediate offset from one lane base), then the LDS image
-// of the output layers, the tree blocks, the UCB / reciprocal tables and the path
 constexpr size_t kSmBytes = (sizeof(MzhOneSmem) + 127) & ~(size_t)127;
 constexpr size_t kL2Bytes = (size_t)MZH_ONE_L2F4 * 16;
 constexpr size_t kTreeOff = kSmBytes + kL2Bytes;
 
 // y = sum_k x[k] * W[k][lane] over K = 256 as one k-ordered fmaf chain from 0 (oracle `linear`): W from the
 // LDS image ([64 k4][NL lanes] float4), x from LDS (one broadcast ds_read_b128 per 4 k-steps)
+// 16 k-steps of a dot-product chain, acc = fmaf(x[16v + j], w[j], acc) for j = 0..15 in order: x comes from
+// lane j of the lane's own 16-lane row (DPP row_newbcast:j -- every row holds x[16v .. 16v + 15], one per lane), so
+// a k-step is ONE v_fmac_f32 with no LDS read for the broadcast operand.  Wait states the compiler cannot see
+// inside the asm: 2 between a VALU write of xv and its DPP read, 5 between a VALU write of EXEC and a DPP op --
+// s_nop 4 before a chain's first block (it may follow a branch), s_nop 1 before the others.
+#define MZH_FMAC(j, wi) "v_fmac_f32_dpp %0, %1, %" #wi " row_newbcast:" #j " row_mask:0xf bank_mask:0xf\n\t"
+#define MZH_FMA16(NOP)                                                                                            \
+  asm(NOP MZH_FMAC(0, 2) MZH_FMAC(1, 3) MZH_FMAC(2, 4) MZH_FMAC(3, 5) MZH_FMAC(4, 6) MZH_FMAC(5, 7) MZH_FMAC(6, 8)      \
+          MZH_FMAC(7, 9) MZH_FMAC(8, 10) MZH_FMAC(9, 11) MZH_FMAC(10, 12) MZH_FMAC(11, 13) MZH_FMAC(12, 14)          \
+              MZH_FMAC(13, 15) MZH_FMAC(14, 16) MZH_FMAC(15, 17)                                                    \
+      : "+v"(acc)                                                                                                   \
+      : "v"(xv), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]), "v"(w[8]), \
+        "v"(w[9]), "v"(w[10]), "v"(w[11]), "v"(w[12]), "v"(w[13]), "v"(w[14]), "v"(w[15]))
+template <bool FIRST = false>
+__device__ __forceinline__ void one_fma16(float& acc, float xv, const float* w) {
+  if constexpr (FIRST)
+    MZH_FMA16("s_nop 4\n\t");
+  else
+    MZH_FMA16("s_nop 1\n\t");
+}
+#undef MZH_FMA16
+#undef MZH_FMAC
+
+// the row layout of a K-vector for one_fma16: lane l holds x[16v + (l & 15)] in xr[v], read from T256 / T64
+template <int NV>
+__device__ __forceinline__ void one_rows(float* xr, const float* xT, int lane) {
+  const float4* r = reinterpret_cast<const float4*>(xT + (lane & 15) * (NV == 16 ? 20 : 4));
+#pragma unroll
+  for (int m = 0; m < NV / 4; ++m) {
+    const float4 q = r[m];
+    xr[4 * m] = q.x;
+    xr[4 * m + 1] = q.y;
+    xr[4 * m + 2] = q.z;
+    xr[4 * m + 3] = q.w;
+  }
+}
+
+// y = sum_k x[k] * W[k][wl] over K = 256 as one k-ordered fmaf chain from 0 (oracle `linear`): W from the
+// LDS image ([64 k4][NL lanes] float4, kept 8 reads ahead), x in the row layout (one_rows).  Every lane of a
+// 16-lane row the DPP broadcast reads from must be active: a disabled source lane disables the FMA.
 template <int NL>
-__device__ __forceinline__ float one_chain256(const float4* w, const float* x, int lane) {
+__device__ __forceinline__ float one_chain256(const float4* w, const float* x, int wl, int lane) {
+  float xr[16];
+  one_rows<16>(xr, x, lane);
+  constexpr int D = 8;
+  float4 wb[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) wb[i] = w[i * NL + wl];
+  // every x read and the first D weight reads issue before the first FMA (LDS completes in issue order: a
+  // block then waits only for its own weights, not for reads issued after them)
+  __builtin_amdgcn_sched_barrier(0);
+  float acc = 0.0f;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    float ww[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 q = wb[(4 * v + i) % D];
+      ww[4 * i] = q.x;
+      ww[4 * i + 1] = q.y;
+      ww[4 * i + 2] = q.z;
+      ww[4 * i + 3] = q.w;
+    }
+    if (v == 0)
+      one_fma16<true>(acc, xr[v], ww);
+    else
+      one_fma16(acc, xr[v], ww);
+    // refill the block's slots with the weights D / 4 blocks ahead, after its FMAs (no copy of the slots)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k4 = 4 * v + i;
+      if (k4 + D < 64) wb[k4 % D] = w[(k4 + D) * NL + wl];
+    }
+  }
+  return acc;
+}
+
+// K = 64 chain with the weight row in registers, x in the row layout
+__device__ __forceinline__ float one_chain64(const float* w, const float* x, int lane) {
+  float xr[4];
+  one_rows<4>(xr, x, lane);
+  float acc = 0.0f;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    if (v == 0)
+      one_fma16<true>(acc, xr[v], w);
+    else
+      one_fma16(acc, xr[v], w + 16 * v);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ float one_relu(float v) { return v > 0.0f ? v : 0.0f; }
+
+// bin 32 of a 33-bin head, chain g (oracle linear_head): fmaf over hidden units k = g, g + 4, ..., g + 252 in order,
+// x from Q[g] and the weights [64] (this lane's MZH_ONE_C32 row), as float4 runs.  A rolled loop (two steps per
+// trip): fully unrolled, the scheduler hoists all 32 reads to the top and the 128 registers they take evict the
+// weight rows the kernel keeps resident.
+__device__ __forceinline__ float one_chain_bin32(const float* q, const float* w) {
+  const float4* x4 = reinterpret_cast<const float4*>(q);
+  const float4* w4 = reinterpret_cast<const float4*>(w);
   float acc = 0.0f;
 #pragma unroll 2
-  for (int k4 = 0; k4 < 64; ++k4) {
-    const float4 wv = w[k4 * NL + lane];
-    const float4 xv = reinterpret_cast<const float4*>(x)[k4];
+  for (int m = 0; m < 16; ++m) {
+    const float4 xv = x4[m], wv = w4[m];
     acc = __builtin_fmaf(xv.x, wv.x, acc);
     acc = __builtin_fmaf(xv.y, wv.y, acc);
     acc = __builtin_fmaf(xv.z, wv.z, acc);
@@ -64,21 +168,88 @@ __device__ __forceinline__ float one_chain256(const float4* w, const float* x, i
   return acc;
 }
 
-// K = 64 chain with the weight row in registers (x from LDS, broadcast)
-__device__ __forceinline__ float one_chain64(const float* w, const float* x) {
-  float acc = 0.0f;
+// The heads (networks.py:83,109,152-189) of mzh_heads_row with its two 33-bin heads on two 8-lane groups
+// instead of side by side on one: lanes 0-7 the value head (and the policy softmax), lanes 8-15 the reward head
+// (and a copy of the policy softmax), so one instruction stream serves both.  Every operation and summation
+// order of a head is mzh_heads_row's (oracle sum8_tree; Markstein quotients unless some lane of the wave flags
+// an argument below -65, then IEEE division everywhere -- equal results wherever the Markstein quotient is
+// exact).  Called by lanes 0-15 of one wave; lanes 0-7 get pp (lane q's prior), value and reward.
+struct OneHeads {
+  float pp, value, reward;
+};
+template <bool SUP33>
+__device__ __forceinline__ OneHeads one_heads(const MzhOneSmem& sm, int l16, bool recurrent) {
+  const int q = l16 & 7;
+  const bool rh = l16 >= 8;
+  const bool live = SUP33 && (!rh || recurrent);  // this group's head feeds a result (mzh_heads_row: h < nh)
+  const float* lv = rh ? sm.lrwd : sm.lval;
+  const float lraw = sm.lpol[q];
+  const float lg = q < MZH_A ? lraw : -__builtin_inff();
+  float e[5], m = -__builtin_inff();
 #pragma unroll
-  for (int k4 = 0; k4 < 16; ++k4) {
-    const float4 xv = reinterpret_cast<const float4*>(x)[k4];
-    acc = __builtin_fmaf(xv.x, w[4 * k4], acc);
-    acc = __builtin_fmaf(xv.y, w[4 * k4 + 1], acc);
-    acc = __builtin_fmaf(xv.z, w[4 * k4 + 2], acc);
-    acc = __builtin_fmaf(xv.w, w[4 * k4 + 3], acc);
+  for (int i = 0; i < 5; ++i) {
+    const int k = q + 8 * i;
+    e[i] = (live && k < 33) ? lv[k] : -__builtin_inff();
+    m = __builtin_fmaxf(e[i], m);
   }
-  return acc;
+  const float mp = mzh_max8_nonan(lg);
+  m = mzh_max8_nonan(m);
+  const float xp = lg - mp;
+  const float epx = mzh_expf_np(xp);
+  const float ep = q < MZH_A ? epx : 0.0f;
+  float xmin = q < MZH_A ? xp : 0.0f;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const float xv = e[i] - m;
+    const float ex = mzh_expf_np(xv);
+    e[i] = (q + 8 * i < 33) ? ex : 0.0f;
+    if (live && q + 8 * i < 33) xmin = __builtin_fminf(xv, xmin);
+  }
+  float a = e[0];
+#pragma unroll
+  for (int i = 1; i < 4; ++i) a = a + e[i];
+  if (q == 0) a = a + e[4];
+  const float sp = mzh_sum8(ep);
+  const float sh = mzh_sum8(a);
+  const bool slow = xmin < -65.0f;
+  auto mdiv = [](float x, float b, float y) {
+    const float qq = x * y;
+    const float rr = __builtin_fmaf(-qq, b, x);
+    return __builtin_fmaf(rr, y, qq);
+  };
+  float pp = mdiv(ep, sp, 1.0f / sp), pk[5];
+  const float y = 1.0f / sh;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) pk[i] = mdiv(e[i], sh, y);
+  if (__builtin_expect(__ballot(slow) != 0, 0)) {
+    pp = ep / sp;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) pk[i] = e[i] / sh;
+  }
+  OneHeads out;
+  out.pp = q < MZH_A ? pp : 0.0f;
+  if (SUP33) {
+    float x = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int k = q + 8 * i;
+      if (k < 33) {
+        const float prod = pk[i] * (float)(k - 16);
+        x = i == 0 ? prod : x + prod;
+      }
+    }
+    x = mzh_sum8(x);
+    const float tv = mzh_signed_parabolic(x);
+    out.value = tv;
+    // the reward head's result, from lane q + 8 (row_ror:8)
+    const float tr = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(tv), 0x128, 0xF, 0xF, true));
+    out.reward = recurrent ? tr : 0.0f;
+  } else {  // support 1 (TD_return = False): the raw head outputs
+    out.value = sm.lval[0];
+    out.reward = recurrent ? sm.lrwd[0] : 0.0f;
+  }
+  return out;
 }
-
-__device__ __forceinline__ float one_relu(float v) { return v > 0.0f ? v : 0.0f; }
 
 // normalize_h_state (networks.py:191-196) of the 64 units held one per lane of a full wave: min / max over
 // the wave (exact, order-free), IEEE division as the oracle's normalize_h
@@ -93,14 +264,25 @@ __device__ __forceinline__ float one_normalize64(float h) {
   const float d = (mx - mn) + 9.999999939225290290778502821922302246094e-09f;
   return (h - mn) / d;
 }
+
+// LDS past the output layers: tree blocks | UCB table, RN(1/k) | path snapshots + chain values | path |
+// (LATL) the latents
+struct OneLayout {
+  size_t table, pc, pcv, path, lat, total;
+};
+__host__ __device__ inline OneLayout one_layout(int S, bool latl) {
+  OneLayout L;
+  L.table = kTreeOff + (size_t)(S + 1) * sizeof(MzhBlock);  // tree blocks (block 0 = the root: unused)
+  L.pc = L.table + sizeof(double) * 2 * (size_t)(S + 3);
+  L.pcv = L.pc + sizeof(MzhPathEnt) * (size_t)(S + 1);
+  L.path = L.pcv + sizeof(double) * (size_t)(S + 1);
+  L.lat = (L.path + sizeof(uint16_t) * (size_t)(S + 1) + 15) & ~(size_t)15;
+  L.total = L.lat + (latl ? sizeof(float) * MZH_H * (size_t)(S + 1) : 0);
+  return L;
+}
 }  // namespace
 
-size_t mzh_one_smem_bytes(int S) {
-  size_t b = kTreeOff + (size_t)(S + 1) * sizeof(MzhBlock);  // tree blocks (block 0 = the root: unused)
-  b += sizeof(double) * 2 * (size_t)(S + 3);                   // UCB table, RN(1/k)
-  b += sizeof(uint16_t) * (size_t)(S + 1);                     // selection path
-  return (b + 15) & ~(size_t)15;
-}
+size_t mzh_one_smem_bytes(int S, bool latl) { return (one_layout(S, latl).total + 15) & ~(size_t)15; }
 
 // The root's 8-lane group (wave 0, lanes 0-7; lane c = child slot c) over the LDS tree.  The same operations,
 // in the same order, as MzhTree (mzh_tree.h) -- node.py:53-123's arithmetic in fp64 with the shared helpers --
@@ -110,6 +292,8 @@ struct MzhOneTree {
   MzhRootBlk& rb;
   MzhBlock* tb;
   uint16_t* path;
+  MzhPathEnt* pc;  // [S + 1] the picked child's (W, R, N) at each depth, snapshot by the selection
+  double* pcv;     // [S + 1] the value the backup adds at each depth
   const double* table;
   const double* inv;
   int lane;
@@ -132,7 +316,10 @@ struct MzhOneTree {
     }
     int pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
     int nx = mzh_group_take((Nr & 0xFFFF) | (Xr << 16), c == pick);
-    if (c == pick) path[0] = (uint16_t)pick;
+    if (c == pick) {
+      path[0] = (uint16_t)pick;
+      pc[0] = MzhPathEnt{rb.W[c], rb.R[c], Nr};
+    }
     int depth = 1, e = 0;
     const int cs = c < MZH_A ? c : MZH_A - 1;
     while ((nx >> 16) >= 0) {
@@ -150,7 +337,10 @@ struct MzhOneTree {
       }
       pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
       nx = mzh_group_take(nxc, c == pick);
-      if (c == pick) path[depth] = (uint16_t)(e * 8 + pick);
+      if (c == pick) {
+        path[depth] = (uint16_t)(e * 8 + pick);
+        pc[depth] = MzhPathEnt{Wc, Rc, Nc};
+      }
       depth++;
     }
     rs.depth = depth;
@@ -191,39 +381,35 @@ struct MzhOneTree {
         tb[le].sl[la].R = rew;
       }
     }
-    double lmax = -__builtin_inf(), lmin = __builtin_inf();
+    // the fp64 value chain leaf -> root on every lane (node.py:53-70: W += value, then value = rwd + gamma *
+    // value), from the rewards the selection snapshot; lane j % 8 keeps the value added at depth j
     double v = (double)val;
     for (int j = depth - 1; j >= 0; --j) {
+      const double rw = j == depth - 1 ? (double)rew : (double)pc[j].R;
+      if (c == (j & 7)) pcv[j] = v;
+      v = rw + disc * v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    // the path nodes' updates, lane c for depths c, c + 8, ...: the snapshot (W, N) + the chain value
+    double lmax = -__builtin_inf(), lmin = __builtin_inf();
+    for (int j = c; j < depth; j += 8) {
       const int ent = path[j];
       const int e = j == 0 ? 0 : ent >> 3, a = j == 0 ? ent : ent & 7;
-      double W;
-      int N;
-      float Rn;
+      const MzhPathEnt pe = pc[j];
+      const double rw = j == depth - 1 ? (double)rew : (double)pe.R;
+      const double Wn = pe.W + pcv[j];
+      const int Nn = pe.N + 1;
       if (j == 0) {
-        W = rb.W[a];
-        N = rb.N[a];
-        Rn = rb.R[a];
+        rb.W[a] = Wn;
+        rb.N[a] = Nn;
       } else {
-        W = tb[e].W[a];
-        N = tb[e].sl[a].nx.N;
-        Rn = tb[e].sl[a].R;
+        tb[e].W[a] = Wn;
+        tb[e].sl[a].nx.N = (uint16_t)Nn;
       }
-      const double rw = j == depth - 1 ? (double)rew : (double)Rn;
-      if (c == (j & 7)) {
-        const double Wn = W + v;
-        const int Nn = N + 1;
-        if (j == 0) {
-          rb.W[a] = Wn;
-          rb.N[a] = Nn;
-        } else {
-          tb[e].W[a] = Wn;
-          tb[e].sl[a].nx.N = (uint16_t)Nn;
-        }
-        const double q = rw + disc * mzh_div(Wn, (double)Nn, inv[Nn]);
-        lmax = q > lmax ? q : lmax;
-        lmin = q < lmin ? q : lmin;
-      }
-      v = rw + disc * v;
+      const double q = rw + disc * mzh_div(Wn, (double)Nn, inv[Nn]);
+      lmax = q > lmax ? q : lmax;
+      lmin = q < lmin ? q : lmin;
     }
     {  // the root (rwd = 0.0): every lane holds the same rootW
       const double W = rs.rootW + v;
@@ -308,7 +494,8 @@ __device__ __forceinline__ int one_fresh(int v) {
   return v;
 }
 
-template <bool SUP33, bool MMIN>
+// LATL: the latents in LDS (when the launcher finds room; otherwise in the engine's HBM workspace)
+template <bool SUP33, bool MMIN, bool LATL>
 __global__ __launch_bounds__(512, 2) void mzh_search_one_kernel(MzhNet net, MzhOneNet on, MzhSearchParams p) {
   extern __shared__ __align__(128) unsigned char smem_raw[];
   MzhOneSmem& sm = *reinterpret_cast<MzhOneSmem*>(smem_raw);
@@ -316,11 +503,15 @@ __global__ __launch_bounds__(512, 2) void mzh_search_one_kernel(MzhNet net, MzhO
   const float* l2f = reinterpret_cast<const float*>(smem_raw + kSmBytes);
   MzhBlock* tb = reinterpret_cast<MzhBlock*>(smem_raw + kTreeOff);
   const int S = p.S;
-  double* table = reinterpret_cast<double*>(tb + (S + 1));
+  const OneLayout lay = one_layout(S, LATL);
+  double* table = reinterpret_cast<double*>(smem_raw + lay.table);
   double* inv = table + (S + 3);  // inv[k] = RN(1/k), k <= S + 2
-  uint16_t* path = reinterpret_cast<uint16_t*>(inv + (S + 3));
+  MzhPathEnt* pc = reinterpret_cast<MzhPathEnt*>(smem_raw + lay.pc);
+  double* pcv = reinterpret_cast<double*>(smem_raw + lay.pcv);
+  uint16_t* path = reinterpret_cast<uint16_t*>(smem_raw + lay.path);
+  float* latl = reinterpret_cast<float*>(smem_raw + lay.lat);  // LATL: [S + 1][64]
 
-  const int t = threadIdx.x, wave = t >> 6;
+  const int t = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform (scalar branches)
   const bool A = t < 256;  // waves 0-3: dynamic_net.0 / rwd_net.0 rows; waves 4-7: policy_net.0 / value_net.0
   const __amdgpu_buffer_rsrc_t wres = mzh_rsrc(on.l1);  // every weight array lies in the one packed blob
   const int wbase = 0;
@@ -348,6 +539,7 @@ __global__ __launch_bounds__(512, 2) void mzh_search_one_kernel(MzhNet net, MzhO
   const __amdgpu_buffer_rsrc_t l2res = mzh_rsrc(on.l2), r2res = mzh_rsrc(on.rep2);
   for (int i = t; i < MZH_ONE_L2F4; i += kThreads)
     *reinterpret_cast<floatx4*>(&l2[i]) = mzh_ld4(l2res, 16 * i, 0);
+  for (int i = t; i < (int)(sizeof(MzhOneSmem) / 4); i += kThreads) reinterpret_cast<float*>(&sm)[i] = 0.0f;
   for (int i = t; i < S + 3; i += kThreads) {
     table[i] = i < S + 2 ? p.table[i] : 0.0;
     inv[i] = 1.0 / (double)i;  // IEEE division: correctly rounded
@@ -362,7 +554,7 @@ __global__ __launch_bounds__(512, 2) void mzh_search_one_kernel(MzhNet net, MzhO
     const __amdgpu_buffer_rsrc_t lres = mzh_rsrc(p.htree + (size_t)r * p.E * MZH_H);
     const int tr = one_fresh(t), lane = tr & 63, n = tr & 255, c = lane & 7;
     const bool grp = wave == 0 && lane < 8;  // the root's 8-lane group (tree phases)
-    MzhOneTree tree{p, sm.root, tb, path, table, inv, lane, disc, noised};
+    MzhOneTree tree{p, sm.root, tb, path, pc, pcv, table, inv, lane, disc, noised};
     // ---------------- root: initial_inference (mcts.py:49-50, networks.py:71-94) ----------------
     if (t < 64) sm.obs[lane] = lane < p.in_dim ? p.obs[(size_t)r * p.in_dim + lane] : 0.0f;
     // representation_net.2 into the dynamic_net.2 region (reloaded below, before the first simulation)
@@ -374,14 +566,17 @@ __global__ __launch_bounds__(512, 2) void mzh_search_one_kernel(MzhNet net, MzhO
       const __amdgpu_buffer_rsrc_t r0 = mzh_rsrc(on.rep0);
       float acc = 0.0f;
       for (int k = 0; k < p.in_dim; ++k) acc = __builtin_fmaf(sm.obs[k], mzh_ld1(r0, 4 * n, k * 1024), acc);
-      sm.hidD[n] = one_relu(acc + on.rep0b[n]);
+      sm.hidDT[one_t256(n)] = one_relu(acc + on.rep0b[n]);
     }
     __syncthreads();
     if (wave == 0) {  // representation_net.2 + normalize_h_state
-      const float h = one_chain256<64>(l2 + MZH_ONE_D2, sm.hidD, lane) + on.rep2b[lane];
+      const float h = one_chain256<64>(l2 + MZH_ONE_D2, sm.hidDT, lane, lane) + on.rep2b[lane];
       const float hn = one_normalize64(h);
-      sm.xh[lane] = hn;
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hn), lres, 4 * lane, 0, 0);  // node 0's latent
+      sm.xhT[one_t64(lane)] = hn;
+      if (LATL)
+        latl[lane] = hn;  // node 0's latent
+      else
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hn), lres, 4 * lane, 0, 0);
     }
     __syncthreads();
 #pragma unroll
@@ -389,43 +584,39 @@ __global__ __launch_bounds__(512, 2) void mzh_search_one_kernel(MzhNet net, MzhO
       *reinterpret_cast<floatx4*>(&l2[MZH_ONE_D2 + tr + 512 * i]) =
           mzh_ld4(l2res, 16 * tr, 16 * (MZH_ONE_D2 + 512 * i));
     if (!A) {  // prediction hidden layers
-      float ap = 0.0f, av = 0.0f;
+      float xr[4], ap = 0.0f, av = 0.0f;
+      one_rows<4>(xr, sm.xhT, lane);
 #pragma unroll
-      for (int k4 = 0; k4 < 16; ++k4) {
-        const float4 xv = reinterpret_cast<const float4*>(sm.xh)[k4];
-        ap = __builtin_fmaf(xv.x, w1[4 * k4], ap);
-        av = __builtin_fmaf(xv.x, w2[4 * k4], av);
-        ap = __builtin_fmaf(xv.y, w1[4 * k4 + 1], ap);
-        av = __builtin_fmaf(xv.y, w2[4 * k4 + 1], av);
-        ap = __builtin_fmaf(xv.z, w1[4 * k4 + 2], ap);
-        av = __builtin_fmaf(xv.z, w2[4 * k4 + 2], av);
-        ap = __builtin_fmaf(xv.w, w1[4 * k4 + 3], ap);
-        av = __builtin_fmaf(xv.w, w2[4 * k4 + 3], av);
+      for (int v = 0; v < 4; ++v) {
+        if (v == 0)
+          one_fma16<true>(ap, xr[v], w1);
+        else
+          one_fma16(ap, xr[v], w1 + 16 * v);
+        one_fma16(av, xr[v], w2 + 16 * v);
       }
-      sm.hidP[n] = one_relu(ap + b1a);
-      sm.hidV[n] = one_relu(av + b1b);
+      const float hv = one_relu(av + b1b);
+      sm.hidPT[one_t256(n)] = one_relu(ap + b1a);
+      sm.hidVT[one_t256(n)] = hv;
+      sm.hidVQ[one_q(n)] = hv;
     }
     __syncthreads();
     if (wave == 0 && lane >= 32) {  // value_net.2 bins 0-31
-      const float acc = one_chain256<64>(l2 + MZH_ONE_A2, sm.hidV, lane);
+      const float acc = one_chain256<64>(l2 + MZH_ONE_A2, sm.hidVT, lane, lane);
       sm.lval[lane - 32] = acc + l2f[MZH_ONE_B2 * 4 + 64 + lane];
-    } else if (wave == 1 && lane < 8) {  // policy_net.2
-      const float acc = one_chain256<8>(l2 + MZH_ONE_P2, sm.hidP, lane);
+    } else if (wave == 1 && lane < 16) {  // policy_net.2 (rows 8-15 repeat 0-7: a DPP row needs all 16 lanes)
+      const float acc = one_chain256<8>(l2 + MZH_ONE_P2, sm.hidPT, lane & 7, lane);
       if (lane < MZH_A) sm.lpol[lane] = acc + l2f[MZH_ONE_B2 * 4 + 128 + lane];
     } else if (SUP33 && wave == 2 && lane >= 4 && lane < 8) {  // value bin 32: four chains over k = g mod 4
       const int g = lane & 3;
-      const float* cw = l2f + MZH_ONE_C32 * 4 + lane;
-      float acc = 0.0f;
-#pragma unroll 8
-      for (int i = 0; i < 64; ++i) acc = __builtin_fmaf(sm.hidV[g + 4 * i], cw[8 * i], acc);
+      float acc = one_chain_bin32(sm.hidVQ + 68 * g, l2f + MZH_ONE_C32 * 4 + 64 * lane);
       acc = acc + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc), 0xB1, 0xF, 0xF, true));  // p0+p1 | p2+p3
       acc = acc + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc), 0x4E, 0xF, 0xF, true));
       if (lane == 4) sm.lval[32] = acc + l2f[MZH_ONE_B2 * 4 + 137];
     }
     __syncthreads();
-    MzhRootReg rs;
+    OneHeads ho{0.0f, 0.0f, 0.0f};
+    if (wave == 0 && lane < 16) ho = one_heads<SUP33>(sm, lane, false);
     if (grp) {
-      const MzhHeadOut ho = mzh_heads_row<1, SUP33 ? 33 : 0, false, false>(sm, net, 0, c, support, false);
       // root.expand(prior, h, 0) with optional Dirichlet mixing (mcts.py:57-69, 132-152)
       MzhRootBlk& rb = sm.root;
       const float pr = c < MZH_A ? ho.pp : 0.0f;
@@ -439,6 +630,7 @@ __global__ __launch_bounds__(512, 2) void mzh_search_one_kernel(MzhNet net, MzhO
         v = (double)scaled + p.eps * p.noise[(size_t)r * MZH_A + c];
       }
       rb.P64[c] = v;
+      MzhRootReg rs;
       double mx = -__builtin_inf(), mn = __builtin_inf();
       if (p.minmax_in) {
         mx = p.minmax_in[2 * r];
@@ -457,98 +649,126 @@ __global__ __launch_bounds__(512, 2) void mzh_search_one_kernel(MzhNet net, MzhO
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
       __builtin_amdgcn_wave_barrier();
       if (S > 0) tree.template select<MMIN>(c, rs);
+      if (c == 0) sm.rsv = rs;
     }
     int lsum = 0;  // p.lockstep_levels: this root's selection levels below the root, summed
     if (wave == 0 && S > 0) {
-      const int e = __shfl(rs.leafE, 0), a = __shfl(rs.leafA, 0);
-      lsum += __shfl(rs.depth, 0) - 1;
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      const int e = sm.rsv.leafE, a = sm.rsv.leafA;
+      lsum += sm.rsv.depth - 1;
       // the leaf's parent latent (mcts.py:89-92), stored by this lane
-      sm.xl[lane] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lres, 4 * lane, 4 * MZH_H * e, 0));
+      sm.xlT[one_t64(lane)] =
+          LATL ? latl[e * MZH_H + lane]
+               : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lres, 4 * lane, 4 * MZH_H * e, 0));
       if (lane == 0) sm.act = a;
     }
     __syncthreads();
+    MZH_STAMP_DECL
     for (int s = 0; s < S; ++s) {
       const int ts = one_fresh(t), ls = ts & 63, ns = ts & 255;
       // ---------------- expand via the network (mcts.py:88-106, networks.py:96-150) ----------------
       if (A) {  // dynamic_net.0: 64 latent steps, the one-hot column, bias, ReLU
-        float acc = one_chain64(w1, sm.xl);
         const int a = sm.act;
+        float acc = one_chain64(w1, sm.xlT, ls);
         const float wa = a == 0 ? woh[0] : a == 1 ? woh[1] : a == 2 ? woh[2] : a == 3 ? woh[3] : a == 4 ? woh[4] : woh[5];
         acc = acc + wa;
-        sm.hidD[ns] = one_relu(acc + b1a);
+        sm.hidDT[one_t256(ns)] = one_relu(acc + b1a);
       }
+      MZH_STAMP(1);
       __syncthreads();
+      MZH_STAMP(2);
       if (wave == 0) {  // dynamic_net.2 (K = 256), then normalize_h_state
-        const float hr = one_chain256<64>(l2 + MZH_ONE_D2, sm.hidD, ls) + l2f[MZH_ONE_B2 * 4 + ls];
-        sm.hraw[ls] = hr;
+        const float hr = one_chain256<64>(l2 + MZH_ONE_D2, sm.hidDT, ls, ls) + l2f[MZH_ONE_B2 * 4 + ls];
+        sm.hrawT[one_t64(ls)] = hr;
         const float hn = one_normalize64(hr);
-        sm.xh[ls] = hn;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hn), lres, 4 * ls, 4 * MZH_H * (s + 1), 0);
+        sm.xhT[one_t64(ls)] = hn;
+        if (LATL)
+          latl[(s + 1) * MZH_H + ls] = hn;  // the new node's latent (expanded node s + 1)
+        else
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hn), lres, 4 * ls, 4 * MZH_H * (s + 1), 0);
       }
+      MZH_STAMP(3);
       __syncthreads();
+      MZH_STAMP(4);
       if (A) {  // rwd_net.0 on the un-normalised latent
-        sm.hidR[ns] = one_relu(one_chain64(w2, sm.hraw) + b1b);
+        const float hr = one_relu(one_chain64(w2, sm.hrawT, ls) + b1b);
+        sm.hidRT[one_t256(ns)] = hr;
+        sm.hidRQ[one_q(ns)] = hr;
       } else {  // policy_net.0 / value_net.0 on the normalised latent
-        float ap = 0.0f, av = 0.0f;
+        float xr[4], ap = 0.0f, av = 0.0f;
+        one_rows<4>(xr, sm.xhT, ls);
 #pragma unroll
-        for (int k4 = 0; k4 < 16; ++k4) {
-          const float4 xv = reinterpret_cast<const float4*>(sm.xh)[k4];
-          ap = __builtin_fmaf(xv.x, w1[4 * k4], ap);
-          av = __builtin_fmaf(xv.x, w2[4 * k4], av);
-          ap = __builtin_fmaf(xv.y, w1[4 * k4 + 1], ap);
-          av = __builtin_fmaf(xv.y, w2[4 * k4 + 1], av);
-          ap = __builtin_fmaf(xv.z, w1[4 * k4 + 2], ap);
-          av = __builtin_fmaf(xv.z, w2[4 * k4 + 2], av);
-          ap = __builtin_fmaf(xv.w, w1[4 * k4 + 3], ap);
-          av = __builtin_fmaf(xv.w, w2[4 * k4 + 3], av);
+        for (int v = 0; v < 4; ++v) {
+          if (v == 0)
+            one_fma16<true>(ap, xr[v], w1);
+          else
+            one_fma16(ap, xr[v], w1 + 16 * v);
+          one_fma16(av, xr[v], w2 + 16 * v);
         }
-        sm.hidP[ns] = one_relu(ap + b1a);
-        sm.hidV[ns] = one_relu(av + b1b);
+        const float hv = one_relu(av + b1b);
+        sm.hidPT[one_t256(ns)] = one_relu(ap + b1a);
+        sm.hidVT[one_t256(ns)] = hv;
+        sm.hidVQ[one_q(ns)] = hv;
       }
+      MZH_STAMP(5);
       __syncthreads();
+      MZH_STAMP(6);
       if (wave == 0) {  // rwd_net.2 bins 0-31 (lanes 0-31) | value_net.2 bins 0-31 (lanes 32-63)
-        const float acc = one_chain256<64>(l2 + MZH_ONE_A2, ls < 32 ? sm.hidR : sm.hidV, ls);
+        const float acc = one_chain256<64>(l2 + MZH_ONE_A2, ls < 32 ? sm.hidRT : sm.hidVT, ls, ls);
         const float y = acc + l2f[MZH_ONE_B2 * 4 + 64 + ls];
         if (ls < 32)
           sm.lrwd[ls] = y;
         else
           sm.lval[ls - 32] = y;
-      } else if (wave == 1 && ls < 8) {  // policy_net.2
-        const float acc = one_chain256<8>(l2 + MZH_ONE_P2, sm.hidP, ls);
+      } else if (wave == 1 && ls < 16) {  // policy_net.2 (rows 8-15 repeat 0-7: a DPP row needs all 16 lanes)
+        const float acc = one_chain256<8>(l2 + MZH_ONE_P2, sm.hidPT, ls & 7, ls);
         if (ls < MZH_A) sm.lpol[ls] = acc + l2f[MZH_ONE_B2 * 4 + 128 + ls];
       } else if (SUP33 && wave == 2 && ls < 8) {  // bin 32 of both heads: lane 4h + g runs chain g of head h
         const int g = ls & 3;
-        const float* hid = ls < 4 ? sm.hidR : sm.hidV;
-        const float* cw = l2f + MZH_ONE_C32 * 4 + ls;
-        float acc = 0.0f;
-#pragma unroll 8
-        for (int i = 0; i < 64; ++i) acc = __builtin_fmaf(hid[g + 4 * i], cw[8 * i], acc);
+        float acc = one_chain_bin32((ls < 4 ? sm.hidRQ : sm.hidVQ) + 68 * g, l2f + MZH_ONE_C32 * 4 + 64 * ls);
         acc = acc + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc), 0xB1, 0xF, 0xF, true));
         acc = acc + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc), 0x4E, 0xF, 0xF, true));
         if (ls == 0) sm.lrwd[32] = acc + l2f[MZH_ONE_B2 * 4 + 136];
         if (ls == 4) sm.lval[32] = acc + l2f[MZH_ONE_B2 * 4 + 137];
       }
+      MZH_STAMP(7);
       __syncthreads();
+      MZH_STAMP(8);
       // ---------------- heads, backup (node.py:53-70), the next selection ----------------
+      OneHeads hs{0.0f, 0.0f, 0.0f};
+      if (wave == 0 && ls < 16) hs = one_heads<SUP33>(sm, ls, true);
       if (grp) {
-        const MzhHeadOut ho = mzh_heads_row<1, SUP33 ? 33 : 0, false, false>(sm, net, 0, ls & 7, support, true);
+        const OneHeads ho = hs;
+        MzhRootReg rs = sm.rsv;
+        MZH_STAMP(9);
         tree.backup(ls & 7, s, rs, ho.value, ho.reward, ho.pp);
+        MZH_STAMP(10);
         if (s + 1 < S) {
           __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
           __builtin_amdgcn_wave_barrier();
           tree.template select<MMIN>(ls & 7, rs);
         }
+        if ((ls & 7) == 0) sm.rsv = rs;
+        MZH_STAMP(11);
       }
       if (wave == 0 && s + 1 < S) {
-        const int e = __shfl(rs.leafE, 0), a = __shfl(rs.leafA, 0);
-        lsum += __shfl(rs.depth, 0) - 1;
-        sm.xl[ls] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lres, 4 * ls, 4 * MZH_H * e, 0));
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        const int e = sm.rsv.leafE, a = sm.rsv.leafA;
+        lsum += sm.rsv.depth - 1;
+        sm.xlT[one_t64(ls)] =
+            LATL ? latl[e * MZH_H + ls]
+                 : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lres, 4 * ls, 4 * MZH_H * e, 0));
         if (ls == 0) sm.act = a;
       }
+      MZH_STAMP(12);
       __syncthreads();
+      MZH_STAMP(13);
     }
     // ---------------- results (mcts.py:111-126, 154-176) ----------------
     if (wave == 0 && lane == 0) {
+      const MzhRootReg rs = sm.rsv;
       tree.results(r, rs);
       if (p.lockstep_levels) p.lockstep_levels[r] = lsum;
     }
@@ -556,20 +776,37 @@ __global__ __launch_bounds__(512, 2) void mzh_search_one_kernel(MzhNet net, MzhO
   }
 }
 
-template <bool SUP33, bool MMIN>
+template <bool SUP33, bool MMIN, bool LATL>
 static hipError_t launch_one_t(const MzhNet& net, const MzhOneNet& on, const MzhSearchParams& p, int grid,
                                hipStream_t stream) {
-  const size_t smem = mzh_one_smem_bytes(p.S);
-  const void* fn = reinterpret_cast<const void*>(&mzh_search_one_kernel<SUP33, MMIN>);
+  const size_t smem = mzh_one_smem_bytes(p.S, LATL);
+  const void* fn = reinterpret_cast<const void*>(&mzh_search_one_kernel<SUP33, MMIN, LATL>);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((mzh_search_one_kernel<SUP33, MMIN>), dim3(grid), dim3(kThreads), smem, stream, net, on, p);
+  hipLaunchKernelGGL((mzh_search_one_kernel<SUP33, MMIN, LATL>), dim3(grid), dim3(kThreads), smem, stream, net, on, p);
   return hipGetLastError();
 }
+template <bool SUP33, bool MMIN>
+static hipError_t launch_one_l(const MzhSearchPlan& pl, const MzhNet& net, const MzhOneNet& on, const MzhSearchParams& p,
+                               hipStream_t stream) {
+  return pl.ohl ? launch_one_t<SUP33, MMIN, true>(net, on, p, pl.grid, stream)
+                : launch_one_t<SUP33, MMIN, false>(net, on, p, pl.grid, stream);
+}
 
+// the instantiation the plan names (grid = min(B, 256): one round of workgroups, each persistent over its roots;
+// pl.ohl: the latents in LDS)
 hipError_t mzh_launch_one(const MzhSearchPlan& pl, const MzhNet& net, const MzhOneNet& on, const MzhSearchParams& p,
                           hipStream_t stream) {
-  const int grid = pl.grid;  // min(B, 256): one round of workgroups, each persistent over its roots
-  if (pl.sup33) return pl.mmin ? launch_one_t<true, true>(net, on, p, grid, stream) : launch_one_t<true, false>(net, on, p, grid, stream);
-  return pl.mmin ? launch_one_t<false, true>(net, on, p, grid, stream) : launch_one_t<false, false>(net, on, p, grid, stream);
+  if (pl.sup33) return pl.mmin ? launch_one_l<true, true>(pl, net, on, p, stream) : launch_one_l<true, false>(pl, net, on, p, stream);
+  return pl.mmin ? launch_one_l<false, true>(pl, net, on, p, stream) : launch_one_l<false, false>(pl, net, on, p, stream);
 }
+
+#ifdef MZH_STAMPS
+// diagnostic build only: this file's phase stamps [8 waves][MZH_NSTAMP], read and cleared
+extern "C" int mzh_diag_stamps_one(unsigned long long* host) {
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(mzh_stamp_acc), sizeof(mzh_stamp_acc)) != hipSuccess) return -2;
+  static unsigned long long zero[8][MZH_NSTAMP] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(mzh_stamp_acc), zero, sizeof(zero)) != hipSuccess) return -2;
+  return 0;
+}
+#endif

@@ -13,7 +13,7 @@ import itertools
 import numpy as np
 import torch
 
-from . import engine
+from . import _lib, engine
 from .engine import require_device
 from .staging import Packed
 
@@ -52,9 +52,10 @@ class TowersOfHanoi:
         h["ctr"][0] = self.step_counter
         h["active"][0] = 1
         pk.to_device()
-        engine.env_step(self.discs, self.max_steps, d["state"], d["action"], d["ctr"], d["active"],
-                        goal_peg=self.goal_peg, moved=d["moved"], obs=d["obs"], reward=d["code"], done=d["done"],
-                        illegal=d["illegal"])
+        q = self._ptrs
+        _lib.check(_lib.lib().mzh_env_step(self.discs, self.goal_peg, self.max_steps, 1, q["state"], q["action"],
+                                           q["moved"], q["obs"], q["code"], q["done"], q["illegal"], q["ctr"],
+                                           q["active"], None, _lib.stream_handle(self._dev)), "mzh_env_step")
         pk.to_host()
         self.c_state = tuple(int(x) for x in h["state"][0])
         self.step_counter, self.reset_check = int(h["ctr"][0]), bool(h["active"][0])
@@ -97,6 +98,7 @@ class TowersOfHanoi:
                                ("moved", torch.uint8, (1, n)), ("obs", torch.float32, (1, 3 * n)),
                                ("code", torch.int8, (1,)), ("done", torch.uint8, (1,)),
                                ("illegal", torch.uint8, (1,))], self._dev)
+            self._ptrs = {k: v.data_ptr() for k, v in self._pk.d.items()}  # fixed: the call passes them as is
         return self._pk
 
     def _encode(self, state):

@@ -9,11 +9,13 @@ fused libmzh kernel launch on the GPU (mzh_search).
 `MCTS.run_batch(states, ...)` runs B independent searches in one launch (each root with its own
 MinMaxStats, i.e. B fresh single-root searches), the form the bench and batched self-play use.
 """
+import ctypes
 import warnings
 
 import numpy as np
 import torch
 
+from . import _lib
 from . import rng as _rng
 from .networks import engine_for
 from .staging import Packed
@@ -94,6 +96,8 @@ class MCTS:
         # latent_actions) and before the action draw (mcts.py:120).  So the search runs, its state
         # is kept, no action uniform is drawn, then the ValueError.
         bad_t = not 0.0 <= temperature <= 1.0
+        if not isinstance(network, RecordedNetwork):
+            return self._run_mcts_fast(state, network, temperature, deterministic, S, bad_t)
         noise, tie, u = _rng.predraw(1, deterministic=deterministic, alpha=self.root_dirichlet_alpha,
                                      eps=self.root_exploration_eps, draw_action=not bad_t)
         if bad_t:
@@ -140,6 +144,79 @@ class MCTS:
         if bad_t:
             raise ValueError(f"Expect `temperature` to be in the range [0.0, 1.0], got {temperature}")
         return int(host["action"][0]), host["pi"][0].astype(np.float64), float(host["root_q"][0])
+
+    def _run_mcts_fast(self, state, network, temperature, deterministic, S, bad_t):
+        """run_mcts for a network: the draws go straight into the pinned staging buffer (rng.predraw_into),
+        and the search arguments -- every device pointer of the staging buffers fixed -- are built once per
+        (engine, S, observation width) and only their scalars and optional pointers set per call"""
+        eng = engine_for(network, S, 1)
+        x = np.asarray(state).reshape(-1)
+        pin, pout, a, addrs = self._prepared(eng, S, x.size)
+        h = pin.h
+        noisy, drew_u = _rng.predraw_into(h["noise"], h["tie"], h["u"], deterministic=deterministic,
+                                          alpha=self.root_dirichlet_alpha, eps=self.root_exploration_eps,
+                                          draw_action=not bad_t, addrs=addrs)
+        if bad_t:
+            deterministic, temperature_k = True, 0.0  # the kernel's policy output is discarded
+        else:
+            temperature_k = temperature
+        h["obs"][0] = x
+        mm = h["mm"][0]
+        mm[0] = self.min_max_stats.maximum
+        mm[1] = self.min_max_stats.minimum
+        pin.to_device()
+        a.n_sims = S
+        a.discount = float(self.discount)
+        a.eps = float(self.root_exploration_eps)
+        a.temperature = float(temperature_k)
+        a.deterministic = 1 if deterministic else 0
+        a.flags = _lib.MZH_FLAG_NP1_UCB if self.np1_ucb else 0
+        d = self._pk_ptrs
+        a.noise = d["noise"] if noisy else None
+        a.action_u = d["u"] if drew_u else None
+        pt = eng.pow_table(S, float(temperature_k))
+        a.pow_table = None if pt is None else pt.data_ptr()
+        _lib.check(_lib.lib().mzh_search(eng._h, ctypes.byref(a), _lib.stream_handle(eng.device)), "mzh_search")
+        pout.to_host()
+        host = pout.h
+        self.min_max_stats.maximum = float(host["minmax"][0, 0])
+        self.min_max_stats.minimum = float(host["minmax"][0, 1])
+        L = int(host["latent_len"][0])
+        self._latent_host = [int(m) for m in host["latent"][0, :L]]  # tensors made on first access
+        self.last_extra_ties = int(host["extra_ties"][0])
+        if self.last_extra_ties:
+            warnings.warn("search met an argmax tie beyond the root's first selection: the NumPy RNG stream "
+                          "now differs from the reference's", RuntimeWarning)
+        if bad_t:
+            raise ValueError(f"Expect `temperature` to be in the range [0.0, 1.0], got {temperature}")
+        return int(host["action"][0]), host["pi"][0].astype(np.float64), float(host["root_q"][0])
+
+    def _prepared(self, eng, S, in_dim):
+        """the staging buffers of _packed and a SearchArgs with their device pointers (cached per engine / S)"""
+        pin, pout = self._packed(eng, S, in_dim, False)
+        key = (id(eng), S, in_dim)
+        if getattr(self, "_args_key", None) != key:
+            d, o = pin.d, pout.d
+            self._pk_ptrs = {k: v.data_ptr() for k, v in d.items()}
+            a = _lib.SearchArgs()
+            a.B = 1
+            a.obs = d["obs"].data_ptr()
+            a.tie_idx = d["tie"].data_ptr()
+            a.minmax_in = d["mm"].data_ptr()
+            a.visits = o["visits"].data_ptr()
+            a.root_q = o["root_q"].data_ptr()
+            a.minmax_out = o["minmax"].data_ptr()
+            a.extra_ties = o["extra_ties"].data_ptr()
+            a.action = o["action"].data_ptr()
+            a.pi = o["pi"].data_ptr()
+            a.latent = o["latent"].data_ptr()
+            a.latent_len = o["latent_len"].data_ptr()
+            a.sel_steps = o["sel_steps"].data_ptr()
+            h = pin.h
+            self._args = a
+            self._addrs = (h["noise"].ctypes.data, h["tie"].ctypes.data, h["u"].ctypes.data)
+            self._args_key = key
+        return pin, pout, self._args, self._addrs
 
     def return_latent_actions(self):
         return self.latent_actions

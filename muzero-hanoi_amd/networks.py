@@ -146,9 +146,38 @@ def _param_signature(net):
     return tuple((p.data_ptr(), p._version) for p in net.parameters())
 
 
+def _param_refs(net):
+    """(module, name) of every parameter, in state_dict order: the signature reads them through the module each
+    call, so a replaced Parameter object is seen as well as an in-place update"""
+    refs = []
+    for mname, mod in net.named_modules():
+        for pname, prm in mod._parameters.items():
+            if prm is not None:
+                refs.append((mod, pname))
+    return refs
+
+
+def _fast_signature(refs):
+    out = []
+    for mod, name in refs:
+        p = mod._parameters[name]
+        out.append(p.data_ptr())
+        out.append(p._version)
+    return tuple(out)
+
+
 def engine_for(net, max_sims, max_roots, device=None):
     """The libmzh engine bound to `net` (ours or any module with MuZeroNet's state_dict keys),
-    with capacity >= (max_sims, max_roots) and the network's CURRENT weights loaded."""
+    with capacity >= (max_sims, max_roots) and the network's CURRENT weights loaded.
+
+    Per call (MCTS.run_mcts makes one per environment step) only the capacity and the parameters' storage /
+    version counters are checked: the shape validation and the parameter list are cached per network."""
+    cache = _CACHE.get(net)
+    if cache is not None and "refs" in cache:
+        eng = cache.get("engine")
+        if eng is not None and eng.max_sims >= max_sims and eng.max_roots >= max_roots:
+            if cache.get("sig") == _fast_signature(cache["refs"]):
+                return eng
     sd_keys = set(net.state_dict().keys())
     missing = [k for k in _engine.WEIGHT_KEYS if k not in sd_keys]
     if missing:
@@ -168,7 +197,9 @@ def engine_for(net, max_sims, max_roots, device=None):
                              max(max_roots, 1 if eng is None else eng.max_roots), support, device=device)
         cache["engine"] = eng
         cache["sig"] = None
-    sig = _param_signature(net)
+    if "refs" not in cache:
+        cache["refs"] = _param_refs(net)
+    sig = _fast_signature(cache["refs"])
     if cache.get("sig") != sig:
         eng.load_weights(_engine.flat_weights(net.state_dict()))
         cache["sig"] = sig

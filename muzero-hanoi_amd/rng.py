@@ -112,6 +112,57 @@ def _predraw_c(rs, n_roots, *, deterministic, alpha, eps, draw_action):
     return noise, tie, u
 
 
+_ALPHAS = {}
+_STATE_ADDR = {}
+
+
+def predraw_into(noise, tie, u, *, deterministic, alpha, eps=0.25, draw_action=True, addrs=None):
+    """`predraw` for the one-root drop-in (MCTS.run_mcts, once per environment step) from the global legacy
+    stream, written straight into the caller's arrays (numpy views of the pinned staging buffer): noise [1,6]
+    f64, tie [1] i32, u [1] f64 -- each drawn only where `predraw` would draw it, the others left untouched.
+    The same C restatement and the same lock; the per-call Python work (allocations, pointer conversions, the
+    bit generator's state address) is cached.  addrs: the three arrays' data addresses, if the caller keeps them.
+    Returns (noise drawn, u drawn)."""
+    rs = np.random.mtrand._rand
+    bg = rs._bit_generator
+    if type(bg).__name__ != "MT19937":
+        n2, t2, u2 = predraw(1, deterministic=deterministic, alpha=alpha, eps=eps, draw_action=draw_action)
+        tie[...] = t2
+        if n2 is not None:
+            noise[...] = n2
+        if u2 is not None:
+            u[...] = u2
+        return n2 is not None, u2 is not None
+    _self_check()
+    from . import _lib
+
+    noisy = uses_noise(deterministic, alpha, eps)
+    draw_u = not deterministic and draw_action
+    key = float(alpha)
+    al = _ALPHAS.get(key)
+    if al is None:
+        al = _alphas(alpha).astype(np.float64)
+        _ALPHAS[key] = al
+    if noisy and (not (al > 0).all() or float(al[0]) > 1.0):
+        # alpha <= 0 raises like RandomState.dirichlet; alpha > 1 needs the Gaussian cache: the general path
+        n2, t2, u2 = predraw(1, deterministic=deterministic, alpha=alpha, eps=eps, draw_action=draw_action)
+        tie[...] = t2
+        noise[...] = n2
+        if u2 is not None:
+            u[...] = u2
+        return True, u2 is not None
+    ent = _STATE_ADDR.get(id(bg))
+    if ent is None or ent[0] is not bg:
+        ent = (bg, bg.ctypes.state_address, np.zeros(2, np.float64))
+        _STATE_ADDR[id(bg)] = ent
+    na, ta, ua = addrs if addrs is not None else (noise.ctypes.data, tie.ctypes.data, u.ctypes.data)
+    with bg.lock:
+        st = _lib.lib().mzh_rng_predraw(ent[1], ent[2].ctypes.data, 1, 6 if noisy else 0, al.ctypes.data, 6,
+                                        1 if draw_u else 0, na if noisy else None, ta, ua if draw_u else None)
+    _lib.check(st, "mzh_rng_predraw")
+    return noisy, draw_u
+
+
 def predraw(n_roots, *, deterministic, alpha, eps=0.25, rng=None, draw_action=True):
     """Draw (noise[B,6] f64 | None, tie[B] i32, u[B] f64 | None) from `rng` (default: the global
     legacy NumPy stream), exactly as B sequential run_mcts calls consume it.  draw_action=False: a

@@ -174,3 +174,70 @@ class PortMCTS:
         else:
             action = int(np.random.choice(np.arange(6), p=pi))
         return action, pi, root.Q(), visits
+
+
+class PortHanoi:
+    """env/hanoi.py:11-151 + utils.py:9-25 restated in the reference's own form (tuples, list scans, NumPy one-hot):
+    the host-side TowersOfHanoi.step the reference runs, as the CPU baseline of the env step
+    (tools/bench_env.py).  tests/test_py_port.py checks it against the exhaustive env fixtures."""
+
+    def __init__(self, N, max_steps, init_state_idx=0, goal_peg=2):
+        import itertools
+
+        self.discs, self.n_pegs = N, 3
+        self.states = list(itertools.product(list(range(3)), repeat=N))
+        self.goal = tuple([goal_peg] * N)
+        self.init_state_idx = init_state_idx
+        self.moves = list(itertools.permutations(list(range(3)), 2))
+        self.max_steps = max_steps
+        self.reset_check = False
+        self.step_counter = 0
+
+    @staticmethod
+    def one_hot(x, n):
+        m = np.zeros((len(x), n))
+        m[np.arange(len(x)), x] = 1
+        return m.reshape(-1)
+
+    def reset(self):
+        self.reset_check = True
+        self.c_state = self.states[self.init_state_idx]
+        return self.one_hot(self.c_state, 3)
+
+    def _discs_on_peg(self, peg):
+        return [d for d in range(self.discs) if self.c_state[d] == peg]
+
+    def _move_allowed(self, move):
+        f, t = self._discs_on_peg(move[0]), self._discs_on_peg(move[1])
+        if f:
+            return (min(t) > min(f)) if t else True
+        return False
+
+    def _get_moved_state(self, move):
+        if self._move_allowed(move):
+            d = min(self._discs_on_peg(move[0]))
+        s = list(self.c_state)
+        s[d] = move[1]
+        return tuple(s)
+
+    def step(self, action):
+        assert self.reset_check, "Need to reset env before taking a step"
+        move = self.moves[action]
+        illegal = not self._move_allowed(move)
+        self.step_counter += 1
+        if not illegal:
+            moved = self._get_moved_state(move)
+            if moved != self.goal:
+                rwd, done = 0, False
+                self.c_state = moved
+            else:
+                rwd, done = 100, True
+                self.reset_check = False
+                self.step_counter = 0
+        else:
+            rwd, moved, done = -100 / 1000, self.c_state, False
+        if self.step_counter == self.max_steps:
+            done = True
+            self.reset_check = False
+            self.step_counter = 0
+        return self.one_hot(moved, 3), rwd, done, illegal

@@ -37,3 +37,19 @@ def test_port_end_to_end_equals_reference(case):
         a, pi, q, visits = m.run_mcts(g["obs"][b], net, float(g["temperature"]), bool(g["deterministic"]))
         assert np.array_equal(visits, g["visits"][b])
         assert q == g["rootQ"][b] and a == g["action"][b]
+
+
+@pytest.mark.parametrize("n", [3, 4])
+def test_port_hanoi_exhaustive(n):
+    """PortHanoi (the host env step the env bench times as the reference's) equals the reference's exhaustive
+    transition tables: next state, the moved state its observation encodes, reward, done and illegal"""
+    g = golden(f"env_N{n}.npz")
+    env = py_port.PortHanoi(n, 10**9)
+    idx = {s: i for i, s in enumerate(env.states)}
+    for i, st in enumerate(env.states):
+        for a in range(6):
+            env.reset_check, env.step_counter, env.c_state = True, 0, st
+            obs, rwd, done, ill = env.step(a)
+            moved = tuple(int(x) for x in np.argmax(obs.reshape(n, 3), 1))
+            assert idx[env.c_state] == g["next_state"][i, a] and idx[moved] == g["moved_state"][i, a]
+            assert rwd == g["reward"][i, a] and done == g["done"][i, a] and ill == g["illegal"][i, a]
