@@ -67,6 +67,10 @@ const char* mzh_last_error(void);
  * differs from the checked-out sources, and bench / smoke records print it. */
 const char* mzh_build_id(void);
 int mzh_device_count(int* count);
+/* The device address of page-locked host memory (hipHostGetDevicePointer): the one-root drop-in calls
+ * (MCTS.run_mcts, TowersOfHanoi.step) hand their few inputs and outputs to the kernels in pinned host memory
+ * the kernels read and write directly, so a call is one launch and one synchronisation, no copies. */
+int mzh_host_device_pointer(void* host, void** dev);
 
 /* ---------------------------------------------------------------------------------------------
  * Engine.  Replaces the state the reference keeps in Python objects: the MuZeroNet weights

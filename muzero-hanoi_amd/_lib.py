@@ -75,6 +75,7 @@ SIGNATURES = {
     "mzh_build_id": (ctypes.c_char_p, []),
     "mzh_last_error": (ctypes.c_char_p, []),
     "mzh_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "mzh_host_device_pointer": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
     "mzh_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                   ctypes.POINTER(_vp)]),
     "mzh_destroy": (ctypes.c_int, [_vp]),
@@ -158,6 +159,13 @@ def device_count():
     n = ctypes.c_int(0)
     st = lib().mzh_device_count(ctypes.byref(n))
     return n.value if st == MZH_OK else 0
+
+
+def host_device_pointer(addr):
+    """the device address of page-locked host memory at `addr` (mzh_host_device_pointer)"""
+    out = _vp()
+    check(lib().mzh_host_device_pointer(addr, ctypes.byref(out)), "mzh_host_device_pointer")
+    return out.value
 
 
 def ptr(t):

@@ -78,6 +78,13 @@ extern "C" int mzh_device_count(int* count) {
   return MZH_OK;
 }
 
+extern "C" int mzh_host_device_pointer(void* host, void** dev) {
+  if (!host || !dev) return fail(MZH_ERR_ARG, "host_device_pointer: NULL argument");
+  *dev = nullptr;
+  hipError_t e = hipHostGetDevicePointer(dev, host, 0);
+  return e == hipSuccess ? MZH_OK : hip_fail(e, "hipHostGetDevicePointer");
+}
+
 static size_t canonical_size(int in_dim, int support) {
   const size_t H = MZH_LATENT, F = MZH_HIDDEN, A = MZH_ACTIONS;
   size_t s = 0;

@@ -46,7 +46,7 @@ class TowersOfHanoi:
             raise IndexError("list index out of range")
         # inputs down in one copy, the kernel, every output back in one copy (staging.Packed)
         pk = self._packed()
-        h, d = pk.h, pk.d
+        h = pk.h
         h["state"][0] = self.c_state
         h["action"][0] = action
         h["ctr"][0] = self.step_counter
@@ -93,12 +93,14 @@ class TowersOfHanoi:
     def _packed(self):
         if self._pk is None:
             n = self.discs
-            self._pk = Packed([("state", torch.uint8, (1, n)), ("action", torch.int32, (1,)),
-                               ("ctr", torch.int32, (1,)), ("active", torch.uint8, (1,)),
-                               ("moved", torch.uint8, (1, n)), ("obs", torch.float32, (1, 3 * n)),
-                               ("code", torch.int8, (1,)), ("done", torch.uint8, (1,)),
-                               ("illegal", torch.uint8, (1,))], self._dev)
-            self._ptrs = {k: v.data_ptr() for k, v in self._pk.d.items()}  # fixed: the call passes them as is
+            fields = [("state", torch.uint8, (1, n)), ("action", torch.int32, (1,)), ("ctr", torch.int32, (1,)),
+                      ("active", torch.uint8, (1,)), ("moved", torch.uint8, (1, n)), ("obs", torch.float32, (1, 3 * n)),
+                      ("code", torch.int8, (1,)), ("done", torch.uint8, (1,)), ("illegal", torch.uint8, (1,))]
+            try:  # the kernel reads and writes the pinned staging buffer itself: one launch + one sync per step
+                self._pk = Packed(fields, self._dev, zero_copy=True)
+            except RuntimeError:  # no device address for pinned memory here: one copy each way
+                self._pk = Packed(fields, self._dev)
+            self._ptrs = self._pk.dptr  # fixed: the call passes them as is
         return self._pk
 
     def _encode(self, state):

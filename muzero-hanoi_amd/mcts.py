@@ -192,31 +192,38 @@ class MCTS:
         return int(host["action"][0]), host["pi"][0].astype(np.float64), float(host["root_q"][0])
 
     def _prepared(self, eng, S, in_dim):
-        """the staging buffers of _packed and a SearchArgs with their device pointers (cached per engine / S)"""
-        pin, pout = self._packed(eng, S, in_dim, False)
+        """zero-copy staging buffers (the search kernel reads its inputs from and writes its outputs to pinned
+        host memory: a call is one launch and one synchronisation) and a SearchArgs holding their device
+        addresses, cached per (engine, S, observation width)"""
         key = (id(eng), S, in_dim)
         if getattr(self, "_args_key", None) != key:
-            d, o = pin.d, pout.d
-            self._pk_ptrs = {k: v.data_ptr() for k, v in d.items()}
+            fin = [("obs", torch.float32, (1, in_dim)), ("noise", torch.float64, (1, 6)), ("tie", torch.int32, (1,)),
+                   ("u", torch.float64, (1,)), ("mm", torch.float64, (1, 2))]
+            fout = [("visits", torch.int32, (1, 6)), ("root_q", torch.float64, (1,)), ("minmax", torch.float64, (1, 2)),
+                    ("extra_ties", torch.int32, (1,)), ("action", torch.int32, (1,)), ("pi", torch.float64, (1, 6)),
+                    ("latent", torch.int32, (1, S + 1)), ("latent_len", torch.int32, (1,)),
+                    ("sel_steps", torch.int32, (1,))]
+            try:
+                pin, pout = Packed(fin, eng.device, zero_copy=True), Packed(fout, eng.device, zero_copy=True)
+            except RuntimeError:  # no device address for pinned memory here: one copy each way
+                pin, pout = Packed(fin, eng.device), Packed(fout, eng.device)
+            d, o = pin.dptr, pout.dptr
+            self._pk_ptrs = d
             a = _lib.SearchArgs()
             a.B = 1
-            a.obs = d["obs"].data_ptr()
-            a.tie_idx = d["tie"].data_ptr()
-            a.minmax_in = d["mm"].data_ptr()
-            a.visits = o["visits"].data_ptr()
-            a.root_q = o["root_q"].data_ptr()
-            a.minmax_out = o["minmax"].data_ptr()
-            a.extra_ties = o["extra_ties"].data_ptr()
-            a.action = o["action"].data_ptr()
-            a.pi = o["pi"].data_ptr()
-            a.latent = o["latent"].data_ptr()
-            a.latent_len = o["latent_len"].data_ptr()
-            a.sel_steps = o["sel_steps"].data_ptr()
+            a.obs = d["obs"]
+            a.tie_idx = d["tie"]
+            a.minmax_in = d["mm"]
+            for k, f in (("visits", "visits"), ("root_q", "root_q"), ("minmax_out", "minmax"),
+                         ("extra_ties", "extra_ties"), ("action", "action"), ("pi", "pi"), ("latent", "latent"),
+                         ("latent_len", "latent_len"), ("sel_steps", "sel_steps")):
+                setattr(a, k, o[f])
             h = pin.h
+            self._prep = (pin, pout)
             self._args = a
             self._addrs = (h["noise"].ctypes.data, h["tie"].ctypes.data, h["u"].ctypes.data)
             self._args_key = key
-        return pin, pout, self._args, self._addrs
+        return self._prep[0], self._prep[1], self._args, self._addrs
 
     def return_latent_actions(self):
         return self.latent_actions

@@ -11,8 +11,12 @@ import torch
 
 
 class Packed:
-    def __init__(self, fields, device):
-        """fields: [(name, torch dtype, shape)] -- each field 16-byte aligned"""
+    def __init__(self, fields, device, zero_copy=False):
+        """fields: [(name, torch dtype, shape)] -- each field 16-byte aligned.
+
+        zero_copy: no device buffer -- the kernels read and write the pinned host buffer itself through its
+        device address (`dptr`: field -> device address; mzh_host_device_pointer), so to_device does nothing and
+        to_host only synchronises."""
         self.layout = {}
         off = 0
         for name, dt, shape in fields:
@@ -20,10 +24,21 @@ class Packed:
             self.layout[name] = (off, dt, tuple(shape), n)
             off += (n + 15) & ~15
         self.nbytes = max(off, 16)
-        self.dev = torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
+        self.zero_copy = zero_copy
+        self.device = torch.device(device)
         self.host = torch.zeros(self.nbytes, dtype=torch.uint8, pin_memory=True)
-        self.d = {k: self._view(self.dev, k) for k in self.layout}  # device tensors
         self.h = {k: self._view(self.host, k).numpy() for k in self.layout}  # numpy views of pinned memory
+        if zero_copy:
+            from . import _lib
+
+            base = _lib.host_device_pointer(self.host.data_ptr())
+            self.dev = None
+            self.d = None
+            self.dptr = {k: base + self.layout[k][0] for k in self.layout}
+        else:
+            self.dev = torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
+            self.d = {k: self._view(self.dev, k) for k in self.layout}  # device tensors
+            self.dptr = {k: v.data_ptr() for k, v in self.d.items()}
 
     def _view(self, buf, k):
         off, dt, shape, n = self.layout[k]
@@ -31,9 +46,11 @@ class Packed:
 
     def to_device(self):
         """host fields -> device fields, ordered on the current stream"""
-        self.dev.copy_(self.host, non_blocking=True)
+        if not self.zero_copy:
+            self.dev.copy_(self.host, non_blocking=True)
 
     def to_host(self):
         """device fields -> host fields; returns once they are there"""
-        self.host.copy_(self.dev, non_blocking=True)
-        torch.cuda.current_stream(self.dev.device).synchronize()
+        if not self.zero_copy:
+            self.host.copy_(self.dev, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
