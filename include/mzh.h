@@ -53,7 +53,7 @@ extern "C" {
                                   occ2 instantiation, runs the cooperative replay kernel instead (the plan
                                   names it) */
 #define MZH_FLAG_KERNEL_ONE 128u /* force the latency kernel (mzh_search_one_kernel: one root per workgroup,
-                                    the network stationary on the CU; default for MLP searches of B <= 1024
+                                    the network stationary on the CU; default for MLP searches of B <= 512
                                     roots whose LDS fits).  An error for replay searches, with another kernel
                                     flag, or where its LDS does not fit */
 

@@ -591,7 +591,7 @@ static KernelChoice choose_kernel(int B, uint32_t flags) {
 // the latency path (mzh_one.hip): MLP searches of up to kOneMaxRoots roots take one root per workgroup
 // (persistent over the roots beyond the 256 workgroups of one round) while its LDS fits; a forced kernel
 // flag (or MZH_KERNEL) decides otherwise.  MZH_FLAG_KERNEL_ONE forces it (an error where it cannot run).
-static const int kOneMaxRoots = 1024, kOneGrid = 256;
+static const int kOneMaxRoots = 512, kOneGrid = 256;  // crossover: profiles/r06_one_probe.json
 static bool one_forced_env() {
   static const bool f = [] {
     const char* v = getenv("MZH_KERNEL");

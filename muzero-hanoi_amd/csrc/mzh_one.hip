@@ -100,9 +100,14 @@ __device__ __forceinline__ float one_chain256(const float4* w, const float* x, i
   float xr[16];
   one_rows<16>(xr, x, lane);
   constexpr int D = 8;
-  float4 wb[D];
+  // one base address register, every read an immediate offset from it (laundered: left to itself the compiler
+  // folds the region offset into per-read constants beyond the 64 KiB offset range and rematerialises them)
+  typedef __attribute__((address_space(3))) const floatx4 LdsF4;
+  LdsF4* wp = (LdsF4*)(w + wl);
+  asm volatile("" : "+v"(wp));
+  floatx4 wb[D];
 #pragma unroll
-  for (int i = 0; i < D; ++i) wb[i] = w[i * NL + wl];
+  for (int i = 0; i < D; ++i) wb[i] = wp[i * NL];
   // every x read and the first D weight reads issue before the first FMA (LDS completes in issue order: a
   // block then waits only for its own weights, not for reads issued after them)
   __builtin_amdgcn_sched_barrier(0);
@@ -112,11 +117,11 @@ __device__ __forceinline__ float one_chain256(const float4* w, const float* x, i
     float ww[16];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float4 q = wb[(4 * v + i) % D];
-      ww[4 * i] = q.x;
-      ww[4 * i + 1] = q.y;
-      ww[4 * i + 2] = q.z;
-      ww[4 * i + 3] = q.w;
+      const floatx4 q = wb[(4 * v + i) % D];
+      ww[4 * i] = q[0];
+      ww[4 * i + 1] = q[1];
+      ww[4 * i + 2] = q[2];
+      ww[4 * i + 3] = q[3];
     }
     if (v == 0)
       one_fma16<true>(acc, xr[v], ww);
@@ -126,7 +131,7 @@ __device__ __forceinline__ float one_chain256(const float4* w, const float* x, i
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int k4 = 4 * v + i;
-      if (k4 + D < 64) wb[k4 % D] = w[(k4 + D) * NL + wl];
+      if (k4 + D < 64) wb[k4 % D] = wp[(k4 + D) * NL];
     }
   }
   return acc;
@@ -150,20 +155,36 @@ __device__ __forceinline__ float one_chain64(const float* w, const float* x, int
 __device__ __forceinline__ float one_relu(float v) { return v > 0.0f ? v : 0.0f; }
 
 // bin 32 of a 33-bin head, chain g (oracle linear_head): fmaf over hidden units k = g, g + 4, ..., g + 252 in order,
-// x from Q[g] and the weights [64] (this lane's MZH_ONE_C32 row), as float4 runs.  A rolled loop (two steps per
-// trip): fully unrolled, the scheduler hoists all 32 reads to the top and the 128 registers they take evict the
-// weight rows the kernel keeps resident.
+// x from Q[g] and the weights [64] (this lane's MZH_ONE_C32 row), as float4 runs kept D reads ahead (the chain
+// waits only for its own operands; fully unrolled without the ring, the scheduler hoists all 32 reads and the
+// 128 registers they take evict the weight rows the kernel keeps resident).
 __device__ __forceinline__ float one_chain_bin32(const float* q, const float* w) {
-  const float4* x4 = reinterpret_cast<const float4*>(q);
-  const float4* w4 = reinterpret_cast<const float4*>(w);
+  typedef __attribute__((address_space(3))) const floatx4 LdsF4;
+  LdsF4* xq = (LdsF4*)q;
+  LdsF4* wq = (LdsF4*)w;
+  asm volatile("" : "+v"(xq), "+v"(wq));
+  constexpr int D = 4;
+  floatx4 xb[D], wb[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    xb[i] = xq[i];
+    wb[i] = wq[i];
+  }
   float acc = 0.0f;
-#pragma unroll 2
-  for (int m = 0; m < 16; ++m) {
-    const float4 xv = x4[m], wv = w4[m];
-    acc = __builtin_fmaf(xv.x, wv.x, acc);
-    acc = __builtin_fmaf(xv.y, wv.y, acc);
-    acc = __builtin_fmaf(xv.z, wv.z, acc);
-    acc = __builtin_fmaf(xv.w, wv.w, acc);
+  // rolled by D (ring slots static in the body); the last trip's refills read the 4 float4 past the run, inside
+  // the LDS image (Q's padding, the next row / the bias block) and unused
+#pragma unroll 1
+  for (int m = 0; m < 16; m += D) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const floatx4 xv = xb[i], wv = wb[i];
+      acc = __builtin_fmaf(xv[0], wv[0], acc);
+      acc = __builtin_fmaf(xv[1], wv[1], acc);
+      acc = __builtin_fmaf(xv[2], wv[2], acc);
+      acc = __builtin_fmaf(xv[3], wv[3], acc);
+      xb[i] = xq[m + D + i];
+      wb[i] = wq[m + D + i];
+    }
   }
   return acc;
 }
@@ -252,15 +273,25 @@ __device__ __forceinline__ OneHeads one_heads(const MzhOneSmem& sm, int l16, boo
 }
 
 // normalize_h_state (networks.py:191-196) of the 64 units held one per lane of a full wave: min / max over
-// the wave (exact, order-free), IEEE division as the oracle's normalize_h
+// the wave (exact, order-free: DPP within each 16-lane row, then the gfx950 row swaps across rows -- no LDS
+// crossbar round trips), IEEE division as the oracle's normalize_h.  The raw units are NaN- and -0-free (an FMA
+// chain from +0 plus a bias), so v_min / v_max are the oracle's min / max.
+__device__ __forceinline__ float one_rowswap_min(float v, bool b32) {
+  const auto r = b32 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false)
+                     : __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return mzh_vmin(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float one_rowswap_max(float v, bool b32) {
+  const auto r = b32 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false)
+                     : __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return mzh_vmax(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
 __device__ __forceinline__ float one_normalize64(float h) {
-  float mn = h, mx = h;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const float a = __shfl_xor(mn, off), b = __shfl_xor(mx, off);
-    mn = a < mn ? a : mn;
-    mx = b > mx ? b : mx;
-  }
+  float mn = mzh_min8_nonan(h), mx = mzh_max8_nonan(h), a, b;
+  asm volatile("s_nop 1\n\tv_min_f32_dpp %0, %1, %1 row_mirror row_mask:0xf bank_mask:0xf" : "=v"(a) : "v"(mn));
+  asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %1, %1 row_mirror row_mask:0xf bank_mask:0xf" : "=v"(b) : "v"(mx));
+  mn = one_rowswap_min(one_rowswap_min(a, false), true);
+  mx = one_rowswap_max(one_rowswap_max(b, false), true);
   const float d = (mx - mn) + 9.999999939225290290778502821922302246094e-09f;
   return (h - mn) / d;
 }
@@ -546,7 +577,6 @@ __global__ __launch_bounds__(512, 2) void mzh_search_one_kernel(MzhNet net, MzhO
   }
   const double disc = p.discount;
   const bool noised = p.noise != nullptr;
-  const int support = net.support;
   __syncthreads();
 
   for (int r = blockIdx.x; r < p.B; r += gridDim.x) {

@@ -89,13 +89,15 @@ def test_search_plan_query_names_the_instantiations(lib):
     assert P(4097) == "mzh_search_kernel<32, false, true, true, false>"
     assert P(4096) == "mzh_search_kernel<16, false, true, true, false>"
     assert P(1025) == "mzh_search_kernel<16, false, true, true, false>"
-    # the latency kernel: MLP searches of <= 1,024 roots (one root per workgroup, up to 256 workgroups)
+    # the latency kernel: MLP searches of <= 512 roots (one root per workgroup, up to 256 workgroups;
+    # the crossover with the cooperative kernel, profiles/r06_one_probe.json)
     # (the third argument: the latents in LDS, where they fit -- n_sims up to ~36)
-    assert P(1024) == P(1) == "mzh_search_one_kernel<true, false, false>"
+    assert P(512) == P(1) == "mzh_search_one_kernel<true, false, false>"
+    assert P(513) == "mzh_search_kernel<16, false, true, true, false>"
     assert P(1, minmax_in=True) == "mzh_search_one_kernel<true, true, false>"
     assert P(1, 25) == "mzh_search_one_kernel<true, false, true>"
     assert lib.search_plan(1, 1, 25)["kernel"] == "mzh_search_one_kernel<false, false, true>"
-    pl = lib.search_plan(33, 1000, 25)
+    pl = lib.search_plan(33, 500, 25)
     assert (pl["workgroups"], pl["roots_per_workgroup"], pl["threads_per_workgroup"]) == (256, 1, 512)
     assert lib.search_plan(33, 7, 25)["workgroups"] == 7
     assert P(1, replay=True) == "mzh_search_kernel<16, true, false, true, false>"  # no replay form
