@@ -87,6 +87,20 @@ def price(tag, lv, sidx, G):
         "by total depth (oracle: not computable before the search)": np.argsort(-tot, kind="stable"),
         "by root state, then total depth (oracle)": np.lexsort((-tot, sidx)),
     }
+    # dealt orders: roots ranked by a depth proxy and dealt round-robin over the B / G groups, so every group
+    # holds one root of each depth stratum (spreads the deep roots instead of gathering them)
+    ngr = -(-B // G)
+
+    def dealt(rank):
+        o = np.full(ngr * G, -1, np.int64)
+        o[:B] = rank
+        o = o.reshape(G, ngr).T.ravel()
+        return o[o >= 0] if B % G == 0 else o  # (B % G != 0: not a BASELINE shape)
+
+    orders["dealt by total depth (oracle)"] = dealt(np.argsort(-tot, kind="stable"))
+    # a proxy known before the search: the depth of the root's first k simulations (a short pre-search)
+    for k in (5, 10):
+        orders[f"dealt by the first {k} simulations' depth"] = dealt(np.argsort(-lv[:, :k].sum(1), kind="stable"))
     # a balanced order: states sorted by their mean depth, then dealt so that every group holds roots of
     # one state where possible (same as "by root state" up to the order of the states)
     st_mean = np.array([tot[sidx == k].mean() if (sidx == k).any() else 0 for k in range(sidx.max() + 1)])
