@@ -353,6 +353,7 @@ struct MzhOneTree {
     }
     int depth = 1, e = 0;
     const int cs = c < MZH_A ? c : MZH_A - 1;
+    MZH_LSTAMP_DECL
     while ((nx >> 16) >= 0) {
       e = nx >> 16;
       const int Np = nx & 0xFFFF;
@@ -362,18 +363,36 @@ struct MzhOneTree {
       const double Wc = b.W[cs];
       if (c >= MZH_A) nxc = (int)0xFFFF0000;
       const int Nc = nxc & 0xFFFF;
+#ifdef MZH_STAMPS
+      asm volatile("" ::"v"(nxc), "v"(Rc), "v"(Pc), "v"(Wc));
+#endif
+      MZH_LSTAMP(0);
       {
         const float u = mzh_ucb(Nc, Wc, Rc, (double)Pc, p.np1, table[Np], disc, has, mmin, den, dinv, inv, EXACT);
         ucb = c < MZH_A ? u : -__builtin_inff();
       }
+#ifdef MZH_STAMPS
+      asm volatile("" ::"v"(ucb));
+#endif
+      MZH_LSTAMP(1);
       pick = mzh_group_pick(ucb, c, lane, tie, firstTie, extra);
+#ifdef MZH_STAMPS
+      asm volatile("" ::"v"(pick));
+#endif
+      MZH_LSTAMP(2);
       nx = mzh_group_take(nxc, c == pick);
       if (c == pick) {
         path[depth] = (uint16_t)(e * 8 + pick);
         pc[depth] = MzhPathEnt{Wc, Rc, Nc};
       }
       depth++;
+#ifdef MZH_STAMPS
+      asm volatile("" ::"v"(nx));
+#endif
+      MZH_LSTAMP(3);
+      MZH_LSTAMP_COUNT();
     }
+    MZH_LSTAMP_FLUSH(20);
     rs.depth = depth;
     rs.leafE = e;
     rs.leafA = pick;
@@ -395,6 +414,7 @@ struct MzhOneTree {
   // reward, then the fp64 value chain leaf -> root on every lane, lane j % 8 updating path depth j
   __device__ __forceinline__ void backup(const int c, const int s, MzhRootReg& rs, float val, float rew, float pp) {
     const int enew = s + 1;
+    MZH_LSTAMP_DECL
     if (c < MZH_A) {
       MzhSlot& sl = tb[enew].sl[c];
       *reinterpret_cast<uint32_t*>(&sl.nx) = 0xFFFF0000u;  // N = 0, X = -1
@@ -414,12 +434,17 @@ struct MzhOneTree {
     }
     // the fp64 value chain leaf -> root on every lane (node.py:53-70: W += value, then value = rwd + gamma *
     // value), from the rewards the selection snapshot; lane j % 8 keeps the value added at depth j
+    MZH_LSTAMP(0);
     double v = (double)val;
     for (int j = depth - 1; j >= 0; --j) {
       const double rw = j == depth - 1 ? (double)rew : (double)pc[j].R;
       if (c == (j & 7)) pcv[j] = v;
       v = rw + disc * v;
     }
+#ifdef MZH_STAMPS
+    asm volatile("" ::"v"(v));
+#endif
+    MZH_LSTAMP(1);
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     __builtin_amdgcn_wave_barrier();
     // the path nodes' updates, lane c for depths c, c + 8, ...: the snapshot (W, N) + the chain value
@@ -442,6 +467,10 @@ struct MzhOneTree {
       lmax = q > lmax ? q : lmax;
       lmin = q < lmin ? q : lmin;
     }
+#ifdef MZH_STAMPS
+    asm volatile("" ::"v"(lmax), "v"(lmin));
+#endif
+    MZH_LSTAMP(2);
     {  // the root (rwd = 0.0): every lane holds the same rootW
       const double W = rs.rootW + v;
       const int N = rs.rootN + 1;
@@ -453,6 +482,12 @@ struct MzhOneTree {
     rs.rootN += 1;
     mzh_maxmin8d(lmax, lmin);
     rs.set_mm(lmax > rs.mmax ? lmax : rs.mmax, lmin < rs.mmin ? lmin : rs.mmin);
+#ifdef MZH_STAMPS
+    asm volatile("" ::"v"(rs.dinv));
+#endif
+    MZH_LSTAMP(3);
+    MZH_LSTAMP_COUNT();
+    MZH_LSTAMP_FLUSH(14);
   }
 
   // results of root r (mcts.py:111-126, 154-176): MzhTree::results from the registers / LDS, one lane
