@@ -71,6 +71,9 @@ int mzh_device_count(int* count);
  * (MCTS.run_mcts, TowersOfHanoi.step) hand their few inputs and outputs to the kernels in pinned host memory
  * the kernels read and write directly, so a call is one launch and one synchronisation, no copies. */
 int mzh_host_device_pointer(void* host, void** dev);
+/* Wait for every call issued on `stream` (hipStreamSynchronize): the one-root drop-ins' single synchronisation
+ * per call, without a framework stream object per call. */
+int mzh_stream_synchronize(void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Engine.  Replaces the state the reference keeps in Python objects: the MuZeroNet weights

@@ -75,6 +75,7 @@ SIGNATURES = {
     "mzh_build_id": (ctypes.c_char_p, []),
     "mzh_last_error": (ctypes.c_char_p, []),
     "mzh_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "mzh_stream_synchronize": (ctypes.c_int, [_vp]),
     "mzh_host_device_pointer": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
     "mzh_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                   ctypes.POINTER(_vp)]),
@@ -173,5 +174,28 @@ def ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_DEV_INDEX = {}
+
+
+def _device_index(device):
+    if device is None:
+        return torch.cuda.current_device()
+    i = _DEV_INDEX.get(device)
+    if i is None:
+        d = torch.device(device) if not isinstance(device, int) else torch.device("cuda", device)
+        i = d.index if d.index is not None else -1
+        _DEV_INDEX[device] = i
+    return torch.cuda.current_device() if i < 0 else i
+
+
 def stream_handle(device=None):
+    """torch's current stream on `device` as a raw hipStream_t (the launch stream of every call)"""
+    if _RAW_STREAM is not None:
+        return ctypes.c_void_p(_RAW_STREAM(_device_index(device)))
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def synchronize(device=None):
+    """wait for the current stream on `device` (mzh_stream_synchronize on the same raw handle the calls use)"""
+    check(lib().mzh_stream_synchronize(stream_handle(device)), "mzh_stream_synchronize")

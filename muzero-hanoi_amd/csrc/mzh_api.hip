@@ -85,6 +85,11 @@ extern "C" int mzh_host_device_pointer(void* host, void** dev) {
   return e == hipSuccess ? MZH_OK : hip_fail(e, "hipHostGetDevicePointer");
 }
 
+extern "C" int mzh_stream_synchronize(void* stream) {
+  hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? MZH_OK : hip_fail(e, "hipStreamSynchronize");
+}
+
 static size_t canonical_size(int in_dim, int support) {
   const size_t H = MZH_LATENT, F = MZH_HIDDEN, A = MZH_ACTIONS;
   size_t s = 0;

@@ -158,12 +158,7 @@ def _param_refs(net):
 
 
 def _fast_signature(refs):
-    out = []
-    for mod, name in refs:
-        p = mod._parameters[name]
-        out.append(p.data_ptr())
-        out.append(p._version)
-    return tuple(out)
+    return tuple([x for mod, name in refs for p in (mod._parameters[name],) for x in (p.data_ptr(), p._version)])
 
 
 def engine_for(net, max_sims, max_roots, device=None):

@@ -9,6 +9,8 @@ one copy and its outputs come back in one copy and one synchronisation.
 import numpy as np
 import torch
 
+from . import _lib
+
 
 class Packed:
     def __init__(self, fields, device, zero_copy=False):
@@ -29,8 +31,6 @@ class Packed:
         self.host = torch.zeros(self.nbytes, dtype=torch.uint8, pin_memory=True)
         self.h = {k: self._view(self.host, k).numpy() for k in self.layout}  # numpy views of pinned memory
         if zero_copy:
-            from . import _lib
-
             base = _lib.host_device_pointer(self.host.data_ptr())
             self.dev = None
             self.d = None
@@ -53,4 +53,4 @@ class Packed:
         """device fields -> host fields; returns once they are there"""
         if not self.zero_copy:
             self.host.copy_(self.dev, non_blocking=True)
-        torch.cuda.current_stream(self.device).synchronize()
+        _lib.synchronize(self.device)
