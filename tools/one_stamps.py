@@ -55,9 +55,11 @@ def main():
     sub = {}
     for name, base, parts in (("backup", 14, ("init+link", "value chain", "path updates", "root+minmax")),
                               ("select_level", 20, ("block load", "ucb", "pick", "take+path")),
-                              ("heads", 25, ("load+max", "exp", "sums+div", "expectation+transform"))):
+                              ):
         cnt = float(buf[0, base + 4])
-        sub[name] = {"count": cnt, **{k: round(float(buf[0, base + i]) / max(cnt, 1.0), 1) for i, k in enumerate(parts)}}
+        if cnt:  # the groups the diagnostic build instruments (mzh_one.hip MZH_LSTAMP_FLUSH bases)
+            sub[name] = {"count": cnt,
+                         **{k: round(float(buf[0, base + i]) / cnt, 1) for i, k in enumerate(parts)}}
     out = {"disks": n, "sims": S, "roots": B, "sel_steps_per_sim": sel / (a.launches * S), "wave0_sub": sub,
            "ticks_per_sim": {f"wave{w}": {PHASES[k]: round(per[w, k], 1) for k in PHASES} for w in (0, 1, 2, 4)},
            "wave0_total": round(float(per[0, 1:14].sum()), 1)}
