@@ -177,11 +177,13 @@ def predraw(n_roots, *, deterministic, alpha, eps=0.25, rng=None, draw_action=Tr
 
 def synthetic_draws(n_roots, *, deterministic, alpha, eps=0.25, seed=0):
     """Vectorised draws of the same distributions for large synthetic batches.
-    Not stream-compatible with the legacy global RNG; used where no parity claim is made."""
-    g = np.random.default_rng(seed)
+    Not stream-compatible with the legacy global RNG; used where no parity claim is made.
+    Each quantity comes from its own child stream of `seed`, so the draws for n roots are the first n rows of
+    the draws for any larger count (BatchedSelfPlay draws a move's batch before it knows how many envs are left)."""
+    gn, gt, gu = (np.random.default_rng(s) for s in np.random.SeedSequence(seed).spawn(3))
     noise = None
     if uses_noise(deterministic, alpha, eps):
-        noise = g.dirichlet(np.full(6, np.float64(np.float32(alpha))), size=n_roots)
-    tie = g.integers(0, 6, size=n_roots, dtype=np.int32)
-    u = None if deterministic else g.random(n_roots)
+        noise = gn.dirichlet(np.full(6, np.float64(np.float32(alpha))), size=n_roots)
+    tie = gt.integers(0, 6, size=n_roots, dtype=np.int32)
+    u = None if deterministic else gu.random(n_roots)
     return noise, tie, u

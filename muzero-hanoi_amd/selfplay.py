@@ -134,6 +134,11 @@ class BatchedSelfPlay:
         if record_obs:
             rec["obs"] = []
         t = lambda a: None if a is None else torch.as_tensor(a).to(dev)
+        cut = lambda a, m: None if a is None else a[:m]
+        # synthetic draws: a move's batch is drawn on the host while the GPU still runs the previous move, for
+        # that move's count of envs (an upper bound), and cut to the count left once it is known (the draws
+        # of n envs are the first n rows of a larger draw, rng.synthetic_draws)
+        pre = None
         while True:
             idx = active.nonzero().squeeze(1)
             n = int(idx.numel())
@@ -142,8 +147,11 @@ class BatchedSelfPlay:
             if legacy_rng:
                 noise, tie, u = _rng.predraw(n, deterministic=deterministic, alpha=self.alpha, eps=self.eps)
             else:
-                noise, tie, u = _rng.synthetic_draws(n, deterministic=deterministic, alpha=self.alpha, eps=self.eps,
-                                                     seed=int(gen.integers(2**31)))
+                if pre is None:
+                    pre = _rng.synthetic_draws(n, deterministic=deterministic, alpha=self.alpha, eps=self.eps,
+                                               seed=int(gen.integers(2**31)))
+                noise, tie, u = (cut(x, n) for x in pre)
+                pre = None
             rp = None
             if replay:
                 call = self.network.next_call()
@@ -178,6 +186,9 @@ class BatchedSelfPlay:
                 rec["obs"].append(full(sub_obs_in, 0.0, torch.float32))
             obs = obs.index_copy(0, idx, sub_obs)
             active = active.index_copy(0, idx, done == 0)
+            if not legacy_rng and not replay:  # the next move's draws, overlapping this move's kernels
+                pre = _rng.synthetic_draws(n, deterministic=deterministic, alpha=self.alpha, eps=self.eps,
+                                           seed=int(gen.integers(2**31)))
         res = {k: torch.stack(v) if v else torch.empty(0, device=dev) for k, v in rec.items()}
         res["steps"] = steps
         res["illegal"] = illegal_n
