@@ -162,7 +162,7 @@ struct MzhSearchPlan {
   int sup33;   // 33-bin value / reward support (cooperative replay: always 1, one instantiation)
   int mmin;    // cooperative / one: caller-given MinMaxStats bounds (subnormal max - min check)
   int occ2;    // cooperative: mzh_search_occ2_kernel<sup33, mmin> (16-root tile, two workgroups per CU)
-  int one;     // latency path: mzh_search_one_kernel<sup33, mmin> (one root per workgroup)
+  int one;     // latency path: mzh_search_one_kernel<sup33, mmin, ohl> (one root per workgroup)
   int grid;    // one: workgroups (each loops over roots b, b + grid, ...)
 };
 

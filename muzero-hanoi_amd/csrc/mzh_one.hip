@@ -3,12 +3,13 @@
 // What it serves: MCTS.run_mcts as Muzero._play_game calls it -- one root, one search per environment step
 // (Muzero.py:165-174, MCTS/mcts.py:34-126) -- and small root batches.  The cooperative kernel (mzh_search.hip)
 // pads one root to a 16-row MFMA tile and streams the 0.49 MB of weights from L2 through the CU in every
-// simulation; here a simulation is a chain of VALU dot products whose operands never leave the CU:
+// simulation; here a simulation is a chain of VALU dot products whose operands never leave the CU, one
+// v_fmac_f32_dpp (row_newbcast: the activation from lane j of the lane's own 16-lane row) per k-step:
 //   - the hidden layers' weight rows in registers for the whole launch (thread t < 256: unit t of
 //     dynamic_net.0 and rwd_net.0; thread 256 + t: unit t of policy_net.0 and value_net.0), two waves per SIMD;
 //   - the K = 256 output layers in LDS (MzhOneNet::l2, k-major, one ds_read_b128 per 4 k-steps);
-//   - the root's tree (one 128-B MzhBlock per expanded node) in LDS; its latents in the engine's HBM workspace
-//     (each lane re-reads only what it stored itself).
+//   - the root's tree (one 128-B MzhBlock per expanded node) in LDS; its latents in LDS too where they fit
+//     (LATL, n_sims up to ~36), else in the engine's HBM workspace (each lane re-reads only what it stored).
 // Numerics are the oracle's (oracle/mzh_oracle.c): every dot product one k-ordered fmaf chain from 0 with the
 // bias added after (bin 32 of a 33-bin head: four chains over k = g mod 4, ((p0 + p1) + (p2 + p3)) + bias),
 // the one-hot action columns as the one non-zero step of that chain (acc + w: the zero steps add +-0 to a
