@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MZH_ABI_VERSION 5
+#define MZH_ABI_VERSION 6
 
 #define MZH_OK 0
 #define MZH_ERR_ARG (-1)         /* bad argument / shape (ValueError in Python)              */
@@ -276,6 +276,53 @@ typedef struct mzh_train_args {
 int mzh_train_scratch_bytes(int B, int U, int in_dim, int support, size_t* bytes);
 int mzh_train_transpose(const mzh_train_args* args, mzh_stream stream);
 int mzh_train_update(const mzh_train_args* args, mzh_stream stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Prioritised replay with the priorities resident in HBM, for the reference Buffer's defaults
+ * (priority_exponent 1, importance_sampling_exponent 0: Muzero.py:72-78, buffer.py:13-14).
+ *
+ * mzh_replay_sample replaces Buffer.priority_sample's draw and batch (buffer.py:89-112): P = p / np.sum(p)
+ * in float32, np.random.choice(np.arange(n), m, replace=True, p=P) from the uniforms u as RandomState
+ * computes it (float64 cdf, cdf /= cdf[-1], searchsorted(u, side='right')), then the sampled rows.  The
+ * indices equal NumPy's for the same u (np.random.random_sample(m), drawn by the caller).  One workgroup.
+ *   n, m             : len(buffer) and batch_s (n >= 1, m >= 1)
+ *   d_state, U, A    : row widths of the five transition arrays (states [.][d_state], rwds / returns
+ *                      [.][U], actions int64 [.][U], pi [.][U][A])
+ *   prio [n]         : device priorities (16-byte aligned)
+ *   u [m]            : uniforms, device-readable (device or mapped page-locked memory)
+ *   cdf [n]          : float64 workspace
+ *   indx [m]         : sampled indices (out)
+ *   out_* [m][.]     : the sampled rows (out)
+ *   status [2]       : device-written (out): [0] 0 = drawn, 1 = P has a NaN or negative entry (NumPy
+ *                      raises ValueError there; indices and rows are then 0 / row 0); [1] 1 = the cdf
+ *                      came from the exact parallel scan, 0 = from the sequential chain
+ * mzh_replay_set_priorities replaces Buffer.update_priorities (buffer.py:127-134): prio[indx[k]] = values[k]
+ * for k = 0..m-1, the last of repeated indices winning as in NumPy's fancy assignment, unless the
+ * reference's assertion (all values finite, one > 0) fails or an index is outside [0, size): then nothing
+ * is written and status[0] = 1 (assertion) / 2 (index), else 0.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct mzh_replay_args {
+  int32_t n, m, d_state, U, A;
+  const float* prio;
+  const double* u;
+  double* cdf;
+  const float* states;
+  const float* rwds;
+  const int64_t* actions;
+  const float* pi;
+  const float* returns;
+  int64_t* indx;
+  float* out_states;
+  float* out_rwds;
+  int64_t* out_actions;
+  float* out_pi;
+  float* out_returns;
+  int32_t* status;
+} mzh_replay_args;
+
+int mzh_replay_sample(const mzh_replay_args* args, mzh_stream stream);
+int mzh_replay_set_priorities(float* prio, int64_t size, const int64_t* indx, const float* values, int m,
+                              int32_t* status, mzh_stream stream);
 
 #ifdef __cplusplus
 }

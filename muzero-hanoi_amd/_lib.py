@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "libmzh.so")
 LIB_PATH = os.environ.get("MZH_LIB") or DEFAULT_LIB  # MZH_LIB: diagnostic builds
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 MZH_OK = 0
 MZH_ERR_ARG = -1
 MZH_ERR_HIP = -2
@@ -69,6 +69,14 @@ class TrainArgs(ctypes.Structure):
     ]
 
 
+class ReplayArgs(ctypes.Structure):
+    """mirror of struct mzh_replay_args (include/mzh.h)"""
+    _fields_ = [("n", _i32), ("m", _i32), ("d_state", _i32), ("U", _i32), ("A", _i32),
+                ("prio", _vp), ("u", _vp), ("cdf", _vp), ("states", _vp), ("rwds", _vp), ("actions", _vp),
+                ("pi", _vp), ("returns", _vp), ("indx", _vp), ("out_states", _vp), ("out_rwds", _vp),
+                ("out_actions", _vp), ("out_pi", _vp), ("out_returns", _vp), ("status", _vp)]
+
+
 # name -> (restype, argtypes); every symbol include/mzh.h declares
 SIGNATURES = {
     "mzh_abi_version": (ctypes.c_int, []),
@@ -97,6 +105,8 @@ SIGNATURES = {
     "mzh_train_scratch_bytes": (ctypes.c_int, [ctypes.c_int] * 4 + [ctypes.POINTER(ctypes.c_size_t)]),
     "mzh_train_transpose": (ctypes.c_int, [ctypes.POINTER(TrainArgs), _vp]),
     "mzh_train_update": (ctypes.c_int, [ctypes.POINTER(TrainArgs), _vp]),
+    "mzh_replay_sample": (ctypes.c_int, [ctypes.POINTER(ReplayArgs), _vp]),
+    "mzh_replay_set_priorities": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_int, _vp, _vp]),
 }
 
 _lib = None

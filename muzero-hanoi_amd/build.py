@@ -16,7 +16,8 @@ CSRC = os.path.join(HERE, "csrc")
 REPO = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libmzh.so")
 OBJ = os.path.join(HERE, "_obj")
-SOURCES = ["mzh_api.hip", "mzh_search.hip", "mzh_wave.hip", "mzh_one.hip", "mzh_env.hip", "mzh_train.hip"]
+SOURCES = ["mzh_api.hip", "mzh_search.hip", "mzh_wave.hip", "mzh_one.hip", "mzh_env.hip", "mzh_train.hip",
+           "mzh_replay.hip"]
 # host-only sources, compiled by g++ like the NumPy C code they restate (no -march: no FMA; see
 # csrc/mzh_rng.cpp)
 HOST_SOURCES = ["mzh_rng.cpp"]

@@ -927,3 +927,25 @@ extern "C" int mzh_train_update(const mzh_train_args* a, mzh_stream stream) {
   e = mzt_launch_grad_adam(gp, tiles, (hipStream_t)stream);
   return e == hipSuccess ? MZH_OK : hip_fail(e, "train grad/adam kernel launch");
 }
+
+extern "C" int mzh_replay_sample(const mzh_replay_args* a, mzh_stream stream) {
+  if (!a) return fail(MZH_ERR_ARG, "replay_sample: null args");
+  if (a->n < 1 || a->m < 1 || a->m > MZR_MAX_BATCH || a->d_state < 1 || a->U < 1 || a->A < 1)
+    return fail(MZH_ERR_ARG, "replay_sample: bad n=%d m=%d (1..%d) d_state=%d U=%d A=%d", a->n, a->m, MZR_MAX_BATCH,
+                a->d_state, a->U, a->A);
+  if (!a->prio || !a->u || !a->cdf || !a->states || !a->rwds || !a->actions || !a->pi || !a->returns || !a->indx ||
+      !a->out_states || !a->out_rwds || !a->out_actions || !a->out_pi || !a->out_returns || !a->status)
+    return fail(MZH_ERR_ARG, "replay_sample: null pointer");
+  if (reinterpret_cast<uintptr_t>(a->prio) % 16 != 0)
+    return fail(MZH_ERR_ARG, "replay_sample: prio must be 16-byte aligned (float4 loads)");
+  hipError_t e = mzr_launch_sample(*a, (hipStream_t)stream);
+  return e == hipSuccess ? MZH_OK : hip_fail(e, "replay sample launch");
+}
+
+extern "C" int mzh_replay_set_priorities(float* prio, int64_t size, const int64_t* indx, const float* values, int m,
+                                         int32_t* status, mzh_stream stream) {
+  if (!prio || !indx || !values || !status || size < 1 || m < 1)
+    return fail(MZH_ERR_ARG, "replay_set_priorities: bad arguments (size=%lld m=%d)", (long long)size, m);
+  hipError_t e = mzr_launch_set_priorities(prio, size, indx, values, m, status, (hipStream_t)stream);
+  return e == hipSuccess ? MZH_OK : hip_fail(e, "replay set_priorities launch");
+}

@@ -5,6 +5,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "../../include/mzh.h"
+
 // kernel-1 view of the network (names follow networks.py:39-67): every weight both as torch stores
 // it ([out][in]) and transposed ([in][out], suffix T), so that each GEMV direction reads coalesced
 struct MztNet {
@@ -63,3 +65,9 @@ size_t mzt_rows_smem_bytes(int rows, int U);
 hipError_t mzt_launch_rows(int rows, int support, const MztRowParams& p, hipStream_t stream);
 hipError_t mzt_launch_grad_adam(const MztGradParams& P, int n_tiles, hipStream_t stream);
 hipError_t mzt_launch_transpose(const float* W, float* WT, int out, int in, int ldwt, hipStream_t stream);
+
+// prioritised replay on the device (mzh_replay.hip): the draw + gather and the priority write-back
+#define MZR_MAX_BATCH 4096  // batch_s per draw (the sampled indices sit in LDS)
+hipError_t mzr_launch_sample(const mzh_replay_args& a, hipStream_t stream);
+hipError_t mzr_launch_set_priorities(float* prio, long long size, const int64_t* idx, const float* val, int m,
+                                     int32_t* status, hipStream_t stream);

@@ -38,7 +38,7 @@ from .utils import adjust_temperature, organise_transitions
 class Muzero:
     def __init__(self, env, s_space_size, n_action, discount, dirichlet_alpha, n_mcts_simulations, unroll_n_steps,
                  batch_s, TD_return, n_TD_step, lr, buffer_size, priority_replay, device, n_ep_x_loop=1,
-                 n_update_x_loop=1, update_impl="torch", selfplay="sequential"):
+                 n_update_x_loop=1, update_impl="torch", selfplay="sequential", device_sampling=None):
         self.dev = device
         self.env = env
         self.n_ep_x_loop = n_ep_x_loop  # episodes collected per training loop
@@ -53,7 +53,12 @@ class Muzero:
                          batch_s=batch_s, device=device)
         self.networks = MuZeroNet(rpr_input_s=s_space_size, action_s=n_action, lr=lr, TD_return=TD_return,
                                   device=device).to(device)
-        self.buffer = Buffer(buffer_size, unroll_n_steps, d_state=s_space_size, n_action=n_action, device=device)
+        # device_sampling (not in the reference's signature): the prioritised draw and the priority
+        # write-back on the device (buffer.Buffer); by default with the fused update on a GPU
+        if device_sampling is None:
+            device_sampling = update_impl == "fused" and bool(priority_replay) and torch.device(device).type == "cuda"
+        self.buffer = Buffer(buffer_size, unroll_n_steps, d_state=s_space_size, n_action=n_action, device=device,
+                             device_sampling=device_sampling)
         self.priority_replay = priority_replay
         # update_impl (not in the reference's signature): "torch" = the reference's op sequence,
         # "graph" = that sequence replayed as one HIP graph (GraphedUpdate), "fused" = the two-kernel
@@ -398,11 +403,15 @@ class FusedUpdate:
         w = priority_w.float().contiguous() if priority_w is not None else None
         a.obs, a.rwds, a.actions, a.pi, a.returns = (t.data_ptr() for t in ins)
         a.weights = w.data_ptr() if w is not None else None
-        a.new_prio = self.new_prio.data_ptr() if w is not None else None
+        # with the buffer's device sampling the new priorities stay on the device (a new tensor per
+        # update: update_priorities consumes it there); else they go to the host as the reference's do
+        on_dev = w is not None and getattr(self.mz.buffer, "device_sampling", False)
+        newp_t = torch.empty(B, dtype=torch.float32, device=states.device) if on_dev else self.new_prio
+        a.new_prio = newp_t.data_ptr() if w is not None else None
         L.check(L.lib().mzh_train_update(a, stream), "mzh_train_update")
         for p in self.params:  # the kernel wrote the parameters in place: let version trackers know
             increment_version(p)
         self._seen = self._versions()
         means = self.row_loss.mean(0)
-        newp = self.new_prio.cpu().numpy() if w is not None else None
+        newp = None if w is None else (newp_t if on_dev else newp_t.cpu().numpy())
         return newp, means[0], means[1], means[2]

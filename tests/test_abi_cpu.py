@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol(lib):
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(lib.SIGNATURES), "ctypes signature table out of sync with include/mzh.h"
-    assert L.mzh_abi_version() == lib.ABI_VERSION == 5
+    assert L.mzh_abi_version() == lib.ABI_VERSION == 6
 
 
 def _c_offsets(struct, fields, tmp_path):
@@ -172,6 +172,23 @@ def test_train_args_layout_matches_header(lib, tmp_path):
     fields = [f[0] for f in lib.TrainArgs._fields_]
     want = [getattr(lib.TrainArgs, f).offset for f in fields] + [ctypes.sizeof(lib.TrainArgs)]
     assert _c_offsets("mzh_train_args", fields, tmp_path) == want
+
+
+def test_replay_args_layout_matches_header(lib, tmp_path):
+    """ctypes ReplayArgs == struct mzh_replay_args as the C compiler lays it out"""
+    fields = [f[0] for f in lib.ReplayArgs._fields_]
+    want = [getattr(lib.ReplayArgs, f).offset for f in fields] + [ctypes.sizeof(lib.ReplayArgs)]
+    assert _c_offsets("mzh_replay_args", fields, tmp_path) == want
+
+
+def test_replay_argument_errors_are_loud(lib):
+    """mzh_replay_sample / mzh_replay_set_priorities refuse bad shapes before touching a device"""
+    L = lib.lib()
+    a = lib.ReplayArgs()
+    assert L.mzh_replay_sample(ctypes.byref(a), None) == lib.MZH_ERR_ARG
+    a.n, a.m, a.d_state, a.U, a.A = 10, 4097, 9, 5, 6
+    assert L.mzh_replay_sample(ctypes.byref(a), None) == lib.MZH_ERR_ARG and "m=4097" in lib.last_error()
+    assert L.mzh_replay_set_priorities(None, 10, None, None, 4, None, None) == lib.MZH_ERR_ARG
 
 
 def test_errors_without_device_are_loud(lib):

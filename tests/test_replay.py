@@ -1,0 +1,172 @@
+"""Prioritised replay on the device (csrc/mzh_replay.hip, Buffer(device_sampling=True)) against NumPy.
+
+The reference's draw is Buffer.priority_sample (buffer.py:89-112): P = p / np.sum(p) (float32), then
+np.random.choice(np.arange(n), m, replace=True, p=P); its write-back is update_priorities
+(buffer.py:127-134).  CPU tests pin the kernel's algorithm, restated in oracle/replay_ref.py, against
+NumPy itself (np.sum's float32 summation order, the exact integer scan in place of the float64 chain,
+the sampled search); GPU tests hold the device draw to the host Buffer -- which tests/test_training.py
+pins to the reference's own recorded indices -- index for index, row for row, with the global NumPy
+stream in the same position afterwards, and check the write-back's NumPy semantics (the last of
+repeated indices wins) and the reference's errors."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import replay_ref
+
+
+def _prios(g, n, kind):
+    if kind == "uniform":
+        return (g.random(n) + 0.05).astype(np.float32)
+    if kind == "heavy":  # priorities over 4 decades, still on the exact path
+        return (10.0 ** g.uniform(-2, 2, n)).astype(np.float32)
+    if kind == "tiny":  # a few probabilities below 2^-28: NumPy's sequential chain
+        p = (g.random(n) + 0.05).astype(np.float32)
+        p[g.integers(0, n, max(1, n // 100))] = np.float32(1e-9)
+        return p
+    if kind == "zeros":
+        p = (g.random(n) + 0.05).astype(np.float32)
+        p[g.random(n) < 0.3] = 0
+        p[0] = 1.0
+        return p
+    raise ValueError(kind)
+
+
+SIZES = [1, 2, 7, 8, 9, 127, 128, 129, 200, 1000, 4095, 4096, 4097, 8191, 8192, 8193, 16384, 50000, 70001]
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_f32_sum_restatement_equals_numpy(n):
+    """np.sum over float32 = 0 + pairwise sums of 8,192-element buffers (NumPy 2.x), bit for bit"""
+    g = np.random.default_rng(n)
+    for kind in ("uniform", "heavy"):
+        a = _prios(g, n, kind)
+        assert replay_ref.numpy_f32_sum(a) == np.sum(a), kind
+
+
+@pytest.mark.parametrize("kind", ["uniform", "heavy", "tiny", "zeros"])
+@pytest.mark.parametrize("n", [1, 7, 300, 4097, 50000])
+def test_draw_restatement_equals_numpy_choice(n, kind):
+    """the kernel's draw, step by step, picks np.random.choice's indices from the same uniforms"""
+    g = np.random.default_rng(1000 + n)
+    p = _prios(g, n, kind)
+    probs = p / np.sum(p)
+    assert replay_ref.exact_cumsum_applies(probs) == (kind != "tiny" or n == 1)
+    if replay_ref.exact_cumsum_applies(probs):  # the integer scan is NumPy's float64 chain exactly
+        assert np.array_equal(replay_ref.scan_cdf(probs), probs.astype(np.float64).cumsum())
+    np.random.seed(n)
+    want = np.random.choice(np.arange(n), size=300, replace=True, p=probs)
+    np.random.seed(n)
+    u = np.random.random_sample(300)
+    assert np.array_equal(replay_ref.draw(p, u), want)
+
+
+def test_draw_restatement_refuses_what_numpy_refuses():
+    p = np.array([1.0, -0.5, 2.0], np.float32)
+    with pytest.raises(ValueError):
+        np.random.choice(np.arange(3), size=4, p=p / np.sum(p))
+    assert replay_ref.draw(p, np.random.random_sample(4)) is None
+    z = np.zeros(5, np.float32)  # all-zero priorities: 0/0
+    assert replay_ref.draw(z, np.random.random_sample(4)) is None
+
+
+def test_device_sampling_needs_gpu_and_defaults():
+    from muzero_hanoi_amd.buffer import Buffer
+
+    with pytest.raises(ValueError):
+        Buffer(10, 5, d_state=9, n_action=6, device="cpu", device_sampling=True)
+
+
+# ------------------------------------------------------------------------------------------- GPU
+def _pair(size, fill, seed, kind):
+    """a host-sampling and a device-sampling Buffer holding the same transitions"""
+    from muzero_hanoi_amd.buffer import Buffer
+
+    g = np.random.default_rng(seed)
+    bufs = [Buffer(size, 5, d_state=9, n_action=6, device="cuda", device_sampling=d) for d in (False, True)]
+    T = fill
+    st = np.zeros((T, 9), np.float32)
+    st[np.arange(T), g.integers(0, 9, T)] = 1
+    data = (st, g.normal(size=(T, 5)).astype(np.float32), g.integers(0, 6, (T, 5)),
+            g.dirichlet(np.ones(6), size=(T, 5)).astype(np.float32), g.normal(size=(T, 5)).astype(np.float32),
+            _prios(g, T, kind))
+    for b in bufs:
+        for a0 in range(0, T, 3000):  # several adds (the ring wraps when fill > size)
+            b.add(*(x[a0:a0 + 3000] for x in data))
+    return bufs
+
+
+def _host(x):
+    return x.cpu().numpy() if torch.is_tensor(x) else np.asarray(x)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size,fill,kind,m", [(1, 1, "uniform", 4), (300, 200, "uniform", 64), (5000, 7000, "heavy", 256),
+                                              (50000, 50000, "uniform", 256), (50000, 50000, "tiny", 256),
+                                              (70001, 70001, "zeros", 4096), (20000, 12345, "heavy", 1)])
+def test_device_draw_equals_host_draw(size, fill, kind, m):
+    host, dev = _pair(size, fill, size + m, kind)
+    assert np.array_equal(dev.priorities, host.priorities)
+    for step in range(3):
+        np.random.seed(step)
+        h = host.priority_sample(m)
+        after_h = np.random.random_sample()
+        np.random.seed(step)
+        d = dev.priority_sample(m)
+        after_d = np.random.random_sample()
+        assert after_h == after_d  # the global stream advanced by the same draws
+        assert np.array_equal(_host(d[5]), _host(h[5])), step
+        for x, y in zip(d[:5], h[:5]):
+            assert torch.equal(x, y)
+        assert torch.equal(d[6], h[6].float())
+        st = dev._dev_replay.status_np[(dev._dev_replay.slot - 1) % dev._dev_replay.RING]
+        torch.cuda.synchronize()
+        assert st[1] == int(kind != "tiny")  # which cumsum path ran
+        newp = (np.random.default_rng(step).random(m) + 0.01).astype(np.float32)
+        host.update_priorities(h[5], newp)
+        dev.update_priorities(d[5], torch.from_numpy(newp).cuda())
+        assert np.array_equal(dev.priorities, host.priorities)
+
+
+@pytest.mark.gpu
+def test_device_update_priorities_numpy_semantics_and_errors():
+    host, dev = _pair(100, 100, 3, "uniform")
+    idx = np.array([5, 7, 5, 9, 7, 5], np.int64)  # repeated indices: the last value stays
+    val = np.arange(1, 7, dtype=np.float32)
+    host.update_priorities(idx, val)
+    dev.update_priorities(torch.from_numpy(idx).cuda(), torch.from_numpy(val).cuda())
+    assert np.array_equal(dev.priorities, host.priorities)
+    before = dev.priorities.copy()
+    for bad in ([np.nan, 1, 1, 1, 1, 1], [0, 0, 0, 0, 0, 0], [np.inf, 1, 1, 1, 1, 1]):
+        bad = np.array(bad, np.float32)
+        with pytest.raises(AssertionError):
+            host.update_priorities(idx, bad)
+        with pytest.raises(AssertionError, match="finite and positive"):
+            dev.update_priorities(idx, bad)
+        assert np.array_equal(dev.priorities, before)  # nothing written
+    with pytest.raises(IndexError):
+        dev.update_priorities(np.array([3, 100]), np.array([1, 1], np.float32))
+    ro = dev.priorities
+    with pytest.raises(ValueError):
+        ro[0] = 1.0  # a read-only copy: writes go through the setter
+    dev.priorities = np.full(100, 2.0, np.float32)
+    assert (dev.priorities == 2.0).all()
+
+
+@pytest.mark.gpu
+def test_device_draw_refuses_what_numpy_refuses():
+    from muzero_hanoi_amd.buffer import Buffer
+
+    dev = Buffer(10, 5, d_state=9, n_action=6, device="cuda", device_sampling=True)
+    with pytest.raises(ValueError):
+        dev.priority_sample(4)  # empty buffer
+    T = 10
+    dev.add(np.zeros((T, 9), np.float32), np.zeros((T, 5), np.float32), np.zeros((T, 5), np.int64),
+            np.full((T, 5, 6), 1 / 6, np.float32), np.zeros((T, 5), np.float32),
+            np.array([1, 1, -1, 1, 1, 1, 1, 1, 1, 1], np.float32))
+    d = dev.priority_sample(4)
+    with pytest.raises(ValueError, match="not non-negative"):
+        dev.update_priorities(d[5], torch.ones(4, device="cuda"))
+    dev.priorities = np.ones(T, np.float32)
+    d = dev.priority_sample(4)
+    dev.update_priorities(d[5], torch.ones(4, device="cuda"))

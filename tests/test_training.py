@@ -29,6 +29,10 @@ def synthetic_transitions(n, seed, T=70):
     return states, rwds, actions, pi_probs, returns, prios
 
 
+def _host(x):
+    return x.cpu().numpy() if torch.is_tensor(x) else x
+
+
 def run_case(g, device, impl="torch"):
     from muzero_hanoi_amd.muzero import Muzero
 
@@ -57,9 +61,10 @@ def run_case(g, device, impl="torch"):
             indx, w = None, None
         newp, vl, rl, pl = mz._update(s, r, a, p, ret, w)
         buf.update_priorities(indx, newp)
-        out["indx"].append(np.full(int(g["batch_s"]), -1) if indx is None else indx)
+        # with the fused update the buffer draws on the device: indices / new priorities as device tensors
+        out["indx"].append(np.full(int(g["batch_s"]), -1) if indx is None else _host(indx))
         out["isw"].append(np.zeros(int(g["batch_s"]), np.float32) if w is None else w.cpu().numpy())
-        out["new_prio"].append(np.zeros(int(g["batch_s"]), np.float32) if newp is None else newp)
+        out["new_prio"].append(np.zeros(int(g["batch_s"]), np.float32) if newp is None else _host(newp))
         for k, v in (("v_loss", vl), ("r_loss", rl), ("p_loss", pl)):
             out[k].append(float(v))
         flat = torch.cat([v.detach().reshape(-1) for v in mz.networks.state_dict().values()]).double().cpu().numpy()
@@ -117,9 +122,11 @@ def test_update_on_gpu_vs_reference(case, impl):
 
 
 @pytest.mark.gpu
-def test_training_loop_runs_on_gpu():
+@pytest.mark.parametrize("impl", ["torch", "fused"])
+def test_training_loop_runs_on_gpu(impl):
     """Muzero.training_loop (Muzero.py:81-151) end to end: self-play searches on the fused kernel,
-    buffer on the device, updates on PyTorch-ROCm, and the search sees the updated weights."""
+    buffer on the device, updates on PyTorch-ROCm (or the fused HIP update with the draw and the
+    priority write-back on the device), and the search sees the updated weights."""
     from muzero_hanoi_amd.env import TowersOfHanoi
     from muzero_hanoi_amd.muzero import Muzero
 
@@ -127,7 +134,8 @@ def test_training_loop_runs_on_gpu():
     np.random.seed(0)
     mz = Muzero(env=TowersOfHanoi(N=3, max_steps=300), s_space_size=9, n_action=6, discount=0.8, dirichlet_alpha=0.25,
                 n_mcts_simulations=8, unroll_n_steps=5, batch_s=16, TD_return=True, n_TD_step=10, lr=0.002,
-                buffer_size=400, priority_replay=True, device="cuda")
+                buffer_size=400, priority_replay=True, device="cuda", update_impl=impl)
+    assert mz.buffer.device_sampling == (impl == "fused")
     before = {k: v.detach().clone() for k, v in mz.networks.state_dict().items()}
     acc = mz.training_loop(n_loops=17, min_replay_size=0, print_acc=8)
     assert len(acc) == 2 and all(np.isfinite(acc))
@@ -205,7 +213,7 @@ def test_fused_update_after_checkpoint_reload():
     out_r = ref._update(*batch[:5], batch[6])
     for x, y in zip(out_f[1:], out_r[1:]):
         np.testing.assert_allclose(float(x), float(y), rtol=2e-4)
-    np.testing.assert_allclose(out_f[0], out_r[0], rtol=1e-3, atol=1e-3)
+    np.testing.assert_allclose(_host(out_f[0]), out_r[0], rtol=1e-3, atol=1e-3)
     pf = torch.cat([v.reshape(-1) for v in fused.networks.state_dict().values()]).cpu().numpy()
     pr = torch.cat([v.reshape(-1) for v in ref.networks.state_dict().values()]).cpu().numpy()
     d = np.abs(pf - pr)

@@ -4,7 +4,9 @@ at the reference's TrainingConfig (training_main.py:15-34: Hanoi N=3, batch 256,
 TD returns, prioritised replay, buffer 50,000, lr 0.002), on synthetic transitions filling the
 buffer.  Legs: the update on the host CPU (the reference's torch op sequence, parity-tested
 against the reference's own fixtures), the eager update on the GPU, the HIP-graph update, and the
-fused two-kernel HIP update (csrc/mzh_train.hip).
+fused two-kernel HIP update (csrc/mzh_train.hip) with the prioritised draw and the priority write-back
+on the device (Buffer(device_sampling=True), csrc/mzh_replay.hip; "fused-hostdraw": the same update with
+the draw on the host in NumPy, as before round 6's device draw).
 
   python tools/bench_train.py [--legs cpu,gpu,graph,fused] [--steps K] [--warmup W] [--batch 256]
 
@@ -53,7 +55,8 @@ def run_leg(leg, args):
     mz = Muzero(env=None, s_space_size=3 * n, n_action=6, discount=0.8, dirichlet_alpha=0.25, n_mcts_simulations=25,
                 unroll_n_steps=5, batch_s=args.batch, TD_return=True, n_TD_step=10, lr=0.002,
                 buffer_size=args.buffer, priority_replay=True, device=dev,
-                update_impl={"cpu": "torch", "gpu": "torch"}.get(leg, leg))
+                update_impl={"cpu": "torch", "gpu": "torch", "fused-hostdraw": "fused"}.get(leg, leg),
+                device_sampling=False if leg == "fused-hostdraw" else None)
     synthetic_fill(mz, n, args.buffer)
     buf = mz.buffer
     sync = torch.cuda.synchronize if dev == "cuda" else (lambda: None)
@@ -84,6 +87,7 @@ def run_leg(leg, args):
     rec = {"metric": "training_updates_per_sec", "leg": leg, "value": steps / dt, "unit": "updates/s",
            "samples_per_sec": steps * args.batch / dt, "ms_per_update": 1e3 * dt / steps,
            "ms_per_update_no_sampling": 1e3 * du / steps, "steps": steps, "warmup": args.warmup,
+           "device_sampling": bool(mz.buffer.device_sampling),
            "final_v_loss": float(vl),
            "config": {"workload": f"hanoi{n}_batch{args.batch}_unroll5_td_prio_buffer{args.buffer}",
                       "device": torch.cuda.get_device_name(0) if dev == "cuda" else "host cpu",
@@ -94,7 +98,7 @@ def run_leg(leg, args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--legs", default="cpu,gpu,graph,fused")
+    ap.add_argument("--legs", default="cpu,gpu,graph,fused,fused-hostdraw")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--cpu-steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
