@@ -182,12 +182,19 @@ __device__ __forceinline__ void copy_row(const uint32_t* __restrict__ src, uint3
 #define MZR_STAMP(i)
 #endif
 
-// one float64 through DPP (both halves; lanes without a source, or outside row_mask, read +0.0)
+// one float64 through DPP (both halves).  ROWS == 0xF: lanes without a source read +0.0 (bound_ctrl);
+// else the rows outside ROWS keep the +0.0 `old`
 template <int CTRL, int ROWS>
 __device__ __forceinline__ double dpp_f64(double v) {
   const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWS, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xF, false);
+  int lo, hi;
+  if (ROWS == 0xF) {
+    lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, ROWS, 0xF, true);
+    hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, ROWS, 0xF, true);
+  } else {
+    lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWS, 0xF, false);
+    hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xF, false);
+  }
   return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
@@ -264,9 +271,10 @@ __global__ __launch_bounds__(RT) void replay_sample_kernel(mzh_replay_args a) {
   int valid = (s > 0.f && s < __builtin_inff()) ? 1 : 0, exact = 1;
   double carry = 0.0;
   static_assert(NS * NWAVE == 64, "one wave scans the wave totals");
-  for (int t0 = 0; t0 < n; t0 += NS * SUB) {
-    const bool whole = t0 + NS * SUB <= n;  // uniform: every element of the tile exists
-    float x[NS][4];                         // elements past n read as 0: P = 0 changes no sum or flag
+  // a tile's elements (those past n read as 0: P = 0 changes no sum or flag); the next tile's are loaded
+  // while this one is processed
+  auto load_tile = [&](int t0, float (&x)[NS][4]) {
+    const bool whole = t0 + NS * SUB <= n;
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
       const int i = t0 + j * SUB + 4 * tid;
@@ -281,13 +289,25 @@ __global__ __launch_bounds__(RT) void replay_sample_kernel(mzh_replay_args a) {
         for (int t = 0; t < 4; ++t) x[j][t] = i + t < n ? p[i + t] : 0.f;
       }
     }
+  };
+  float xn[NS][4];
+  load_tile(0, xn);
+  for (int t0 = 0; t0 < n; t0 += NS * SUB) {
+    const bool whole = t0 + NS * SUB <= n;  // uniform: every element of the tile exists
+    float x[NS][4];
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) x[j][t] = xn[j][t];
+    if (t0 + NS * SUB < n) load_tile(t0 + NS * SUB, xn);
     bool slow = false;
     float q[NS][4];
 #pragma unroll
     for (int j = 0; j < NS; ++j)
 #pragma unroll
       for (int t = 0; t < 4; ++t) q[j][t] = mzh_fdiv(x[j][t], s, y, slow);
-    if (__builtin_amdgcn_ballot_w64(slow) != 0) {
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(slow) != 0, 0)) {
+      asm volatile("" ::: "memory");  // keeps the IEEE divisions behind the branch (not speculated)
 #pragma unroll
       for (int j = 0; j < NS; ++j)
 #pragma unroll
