@@ -170,6 +170,14 @@ class _DeviceReplay:
         self.u_dev = self.L.host_device_pointer(self.u.data_ptr())
         self.ones = torch.ones(m, dtype=torch.float32, device=self.buf.dev)
         self.m = m
+        buf = self.buf
+        a = self.L.ReplayArgs()
+        a.m, a.d_state, a.U, a.A = m, buf.d_state, buf.unroll_n_steps, buf.n_action
+        a.prio, a.cdf = self.prio.data_ptr(), self.cdf.data_ptr()
+        a.states, a.rwds, a.actions = buf.states.data_ptr(), buf.rwds.data_ptr(), buf.actions.data_ptr()
+        a.pi, a.returns = buf.pi_probs.data_ptr(), buf.mc_returns.data_ptr()
+        self.args = a
+        self.args_ptr = ctypes.byref(a)
 
     def check_pending(self, block):
         """raise NumPy's ValueError for a finished draw whose probabilities it would have refused"""
@@ -206,14 +214,13 @@ class _DeviceReplay:
                torch.empty((m, U), dtype=torch.int64, device=dev),
                torch.empty((m, U, A), dtype=torch.float32, device=dev),
                torch.empty((m, U), dtype=torch.float32, device=dev))
-        a = self.L.ReplayArgs()
-        a.n, a.m, a.d_state, a.U, a.A = n, m, buf.d_state, U, A
-        a.prio, a.u, a.cdf = self.prio.data_ptr(), self.u_dev + s * m * 8, self.cdf.data_ptr()
-        a.states, a.rwds, a.actions = buf.states.data_ptr(), buf.rwds.data_ptr(), buf.actions.data_ptr()
-        a.pi, a.returns, a.indx = buf.pi_probs.data_ptr(), buf.mc_returns.data_ptr(), indx.data_ptr()
+        a = self.args  # the fixed fields were set by _alloc_u
+        a.n = n
+        a.u = self.u_dev + s * m * 8
+        a.indx = indx.data_ptr()
         a.out_states, a.out_rwds, a.out_actions, a.out_pi, a.out_returns = (t.data_ptr() for t in out)
         a.status = self.status_dev + s * 8
-        self.L.check(self.L.lib().mzh_replay_sample(ctypes.byref(a), self._stream()), "mzh_replay_sample")
+        self.L.check(self.L.lib().mzh_replay_sample(self.args_ptr, self._stream()), "mzh_replay_sample")
         ev = self.events[s]
         ev.record(torch.cuda.current_stream(dev))
         self.pending[s] = ev

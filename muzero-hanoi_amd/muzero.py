@@ -375,12 +375,15 @@ class FusedUpdate:
         a.scratch_bytes = self.scratch.numel() * 4
         a.row_loss = self.row_loss.data_ptr()
         self._a = a
-        self._steps = [st["step"] for st in states_]
+        # Adam's per-parameter step counters (0-dim host tensors in the optimiser's state): written through
+        # NumPy views (one _foreach_add_ over 20 host tensors costs more than the update's launch)
+        self._step_views = [st["step"].numpy() for st in states_]
         self._state_key = self._state_identity()
 
     def _state_identity(self):
+        # Optimizer.load_state_dict installs a new state dict: its identity (and size) marks a reload
         opt = self.mz.networks.optimiser
-        return (id(opt.state),) + tuple(id(opt.state[p].get("exp_avg")) for p in self.params)
+        return id(opt.state), len(opt.state)
 
     def __call__(self, states, rwds, actions, pi_probs, returns, priority_w):
         L = self._lib
@@ -393,8 +396,7 @@ class FusedUpdate:
             L.check(L.lib().mzh_train_transpose(a, stream), "mzh_train_transpose")
         g = self.mz.networks.optimiser.param_groups[0]
         beta1, beta2 = g["betas"]
-        torch._foreach_add_(self._steps, 1)  # Adam's per-parameter step counters (host tensors)
-        step = float(self._steps[0])
+        step = float(self._step_views[0]) + 1.0  # this update's step (written back after the launch)
         a.step_size = g["lr"] / (1 - beta1 ** step)
         a.bc2_sqrt = math.sqrt(1 - beta2 ** step)
         a.beta1, a.beta2, a.eps = beta1, beta2, g["eps"]
@@ -409,8 +411,9 @@ class FusedUpdate:
         newp_t = torch.empty(B, dtype=torch.float32, device=states.device) if on_dev else self.new_prio
         a.new_prio = newp_t.data_ptr() if w is not None else None
         L.check(L.lib().mzh_train_update(a, stream), "mzh_train_update")
-        for p in self.params:  # the kernel wrote the parameters in place: let version trackers know
-            increment_version(p)
+        for v in self._step_views:  # torch.optim.Adam's step += 1 (float32), while the kernels run
+            v[...] = step
+        increment_version(self.params)  # the kernel wrote the parameters in place: let version trackers know
         self._seen = self._versions()
         means = self.row_loss.mean(0)
         newp = None if w is None else (newp_t if on_dev else newp_t.cpu().numpy())
