@@ -290,7 +290,7 @@ int mzh_train_update(const mzh_train_args* args, mzh_stream stream);
  *                      [.][U], actions int64 [.][U], pi [.][U][A])
  *   prio [n]         : device priorities (16-byte aligned)
  *   u [m]            : uniforms, device-readable (device or mapped page-locked memory)
- *   cdf [n]          : float64 workspace
+ *   cdf [n]          : float64 workspace (the kernel keeps the cdf at every 4th element)
  *   indx [m]         : sampled indices (out)
  *   out_* [m][.]     : the sampled rows (out)
  *   status [2]       : device-written (out): [0] 0 = drawn, 1 = P has a NaN or negative entry (NumPy

@@ -260,8 +260,9 @@ __global__ __launch_bounds__(RT) void replay_sample_kernel(mzh_replay_args a) {
   MZR_STAMP(2)
 
   // ---- P_i = p_i / s and the cdf in one pass.  A sub-tile is 4 consecutive elements per lane over the
-  // workgroup (float4 loads and double2 stores coalesce); a lane's running sums, a wave scan and the waves'
-  // totals through LDS give each element's prefix, NS sub-tiles per barrier.  On the exact path every
+  // workgroup (float4 loads coalesce); a lane's sum, a wave scan and the waves' totals through LDS give the
+  // cdf at every 4th element (cdf4, the only values stored: the search replays a group's 4 additions), NS
+  // sub-tiles per barrier.  On the exact path every
   // partial sum of the P_i is a multiple of 2^-51 below 4, so these float64 additions in any order are
   // exact and the prefixes are NumPy's cumsum values; else (or if invalid) the values written here are
   // replaced below.  Quotients by Markstein from y = RN(1/s) (mzh_fdiv: exact unless an operand is tiny,
@@ -293,7 +294,6 @@ __global__ __launch_bounds__(RT) void replay_sample_kernel(mzh_replay_args a) {
   float xn[NS][4];
   load_tile(0, xn);
   for (int t0 = 0; t0 < n; t0 += NS * SUB) {
-    const bool whole = t0 + NS * SUB <= n;  // uniform: every element of the tile exists
     float x[NS][4];
 #pragma unroll
     for (int j = 0; j < NS; ++j)
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(RT) void replay_sample_kernel(mzh_replay_args a) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) q[j][t] = x[j][t] / s;
     }
-    double c[NS][4], run[NS], w[NS];
+    double run[NS], w[NS];
     bool ok = true, ex = true;
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
@@ -324,7 +324,6 @@ __global__ __launch_bounds__(RT) void replay_sample_kernel(mzh_replay_args a) {
         ok &= (v >= 0.f) & (v <= 1.f);  // else NaN, negative, or a sum that overflowed
         ex &= (v == 0.f) | (v >= kMinExact);
         run[j] += (double)v;
-        c[j][t] = run[j];
       }
       w[j] = run[j];
     }
@@ -346,16 +345,9 @@ __global__ __launch_bounds__(RT) void replay_sample_kernel(mzh_replay_args a) {
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
-      const double base = carry + L.wpre[j * NWAVE + wave] + (w[j] - run[j]);  // this lane's exclusive prefix
+      // the cdf at this lane's 4th element (elements past n added 0): cdf4[g] = cdf[min(4g + 3, n - 1)]
       const int i = t0 + j * SUB + 4 * tid;
-      if (whole || i + 4 <= n) {
-        *reinterpret_cast<double2*>(a.cdf + i) = make_double2(base + c[j][0], base + c[j][1]);
-        *reinterpret_cast<double2*>(a.cdf + i + 2) = make_double2(base + c[j][2], base + c[j][3]);
-      } else {
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-          if (i + t < n) a.cdf[i + t] = base + c[j][t];
-      }
+      if (i < n) a.cdf[i >> 2] = carry + L.wpre[j * NWAVE + wave] + w[j];
     }
     carry += L.wpre[64];
   }
@@ -372,11 +364,11 @@ __global__ __launch_bounds__(RT) void replay_sample_kernel(mzh_replay_args a) {
       if (tid == 0) {
         for (int i = 0; i < tn; ++i) {
           c += (double)L.u.f.q[i];
-          L.u.f.c[i] = c;
+          L.u.f.c[i >> 2] = c;  // a group's last write is its 4th element (or element n - 1)
         }
       }
       __syncthreads();
-      for (int i = tid; i < tn; i += RT) a.cdf[t0 + i] = L.u.f.c[i];
+      for (int g = tid; g < (tn + 3) / 4; g += RT) a.cdf[(t0 >> 2) + g] = L.u.f.c[g];
       __syncthreads();
     }
   }
@@ -387,11 +379,14 @@ __global__ __launch_bounds__(RT) void replay_sample_kernel(mzh_replay_args a) {
   __syncthreads();
 
   MZR_STAMP(4)
-  // ---- searchsorted(u, 'right') on cdf / cdf[n-1]: the LDS sample, then the block in HBM
+  // ---- searchsorted(u, 'right') on cdf / cdf[n-1]: the group of 4 from the LDS sample of cdf4 and a window
+  // of cdf4 in HBM, then the element inside the group by replaying its 4 additions from the previous
+  // group's value (NumPy's own chain on either path: exact sums, or the sequential values themselves)
   if (valid) {
-    const double last = a.cdf[n - 1], ylast = 1.0 / last;  // cdf[i] / last by Markstein (rdiv)
-    const int stride = (n + NC - 1) / NC, nc = (n + stride - 1) / stride;
-    for (int jj = tid; jj < nc; jj += RT) L.u.cn[jj] = rdiv(a.cdf[min(n, (jj + 1) * stride) - 1], last, ylast);
+    const int n4 = (n + 3) >> 2;
+    const double last = a.cdf[n4 - 1], ylast = 1.0 / last;  // cdf / last by Markstein (rdiv)
+    const int stride = (n4 + NC - 1) / NC, nc = (n4 + stride - 1) / stride;
+    for (int jj = tid; jj < nc; jj += RT) L.u.cn[jj] = rdiv(a.cdf[min(n4, (jj + 1) * stride) - 1], last, ylast);
     __syncthreads();
     MZR_STAMP(5)
     for (int k = tid; k < m; k += RT) {
@@ -404,22 +399,40 @@ __global__ __launch_bounds__(RT) void replay_sample_kernel(mzh_replay_args a) {
         else
           lo = mid + 1;
       }
-      int i = lo * stride, e = min(n, (lo + 1) * stride) - 1;  // the answer is in [i, e], cdf[e] above uk
-      while (e - i >= LIN) {
-        const int mid = (i + e) >> 1;
+      int g = lo * stride, e = min(n4, (lo + 1) * stride) - 1;  // the group is in [g, e], cdf4[e] above uk
+      while (e - g >= LIN) {
+        const int mid = (g + e) >> 1;
         if (rdiv(a.cdf[mid], last, ylast) > uk)
           e = mid;
         else
-          i = mid + 1;
+          g = mid + 1;
       }
-      double w[LIN];  // the window at once: the answer is i + the number of entries at or below uk
+      double w[LIN];  // the window at once: the group is g + the number of entries at or below uk
 #pragma unroll
-      for (int t = 0; t < LIN; ++t) w[t] = i + t < e ? a.cdf[i + t] : 0.0;
+      for (int t = 0; t < LIN; ++t) w[t] = g + t < e ? a.cdf[g + t] : 0.0;
       int below = 0;
 #pragma unroll
-      for (int t = 0; t < LIN; ++t) below += (i + t < e && !(rdiv(w[t], last, ylast) > uk)) ? 1 : 0;
-      L.sidx[k] = i + below;
-      a.indx[k] = i + below;
+      for (int t = 0; t < LIN; ++t) below += (g + t < e && !(rdiv(w[t], last, ylast) > uk)) ? 1 : 0;
+      g += below;
+      double c = g > 0 ? a.cdf[g - 1] : 0.0;
+      const int i0 = 4 * g, cnt = min(4, n - i0);
+      float x[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) x[t] = t < cnt ? p[i0 + t] : 0.f;
+      int idx = i0 + cnt - 1;  // the group's last element is above uk
+      bool found = false;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (t < cnt && !found) {
+          c += (double)(x[t] / s);
+          if (rdiv(c, last, ylast) > uk) {
+            idx = i0 + t;
+            found = true;
+          }
+        }
+      }
+      L.sidx[k] = idx;
+      a.indx[k] = idx;
     }
   } else {
     for (int k = tid; k < m; k += RT) {
