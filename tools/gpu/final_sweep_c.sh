@@ -1,6 +1,6 @@
 # final pass, part C: the secondary rows (self-play, evaluation, training updates; tools/gpu/secondary.sh), the
 # scalar env step, and the latency path -- crossover probe + run_mcts under rocprofv3 --kernel-trace --stats (the
-# latency kernel's own launch durations), then its phase stamps on the diagnostic build
+# latency kernel's own launch durations), then its phase stamps on the diagnostic build; the replay draw's stamps
 set -e
 R=${GRAFT_REPO_ROOT:-$PWD}
 cd $R
@@ -15,3 +15,6 @@ cd $R
 tail -2 gpurun_out/prof_one.log
 MZH_DIAG_LIB=muzero-hanoi_amd/libmzh_diag.so timeout -k 10 120 python tools/one_stamps.py > gpurun_out/one_stamps.json
 python -c "import json;d=json.load(open('gpurun_out/one_stamps.json'));print('stamps',d['wave0_total'])"
+# the device replay draw: its phase stamps (diagnostic build) and the fused update's host-side split
+MZH_LIB=muzero-hanoi_amd/libmzh_diag.so timeout -k 10 120 python tools/replay_stamps.py --out gpurun_out/replay_stamps.json
+timeout -k 10 200 python tools/train_host_profile.py --out gpurun_out/train_host_profile.json
