@@ -44,19 +44,32 @@ class TowersOfHanoi:
         action = int(action)
         if not 0 <= action < 6:
             raise IndexError("list index out of range")
-        # inputs down in one copy, the kernel, every output back in one copy (staging.Packed)
+        pk = self._launch_step(action=action)
+        pk.to_host()
+        return self._finish_step()
+
+    def _launch_step(self, action=None, action_ptr=None):
+        """stage the env's state and launch mzh_env_step on the current stream; the action either goes into
+        the staging record or is read by the kernel from `action_ptr` (device-readable int32, e.g. the search's
+        own action output: MCTS.run_mcts_step chains the two launches)"""
         pk = self._packed()
         h = pk.h
         h["state"][0] = self.c_state
-        h["action"][0] = action
+        if action_ptr is None:
+            h["action"][0] = action
         h["ctr"][0] = self.step_counter
         h["active"][0] = 1
         pk.to_device()
         q = self._ptrs
-        _lib.check(_lib.lib().mzh_env_step(self.discs, self.goal_peg, self.max_steps, 1, q["state"], q["action"],
-                                           q["moved"], q["obs"], q["code"], q["done"], q["illegal"], q["ctr"],
-                                           q["active"], None, _lib.stream_handle(self._dev)), "mzh_env_step")
-        pk.to_host()
+        _lib.check(_lib.lib().mzh_env_step(self.discs, self.goal_peg, self.max_steps, 1, q["state"],
+                                           q["action"] if action_ptr is None else action_ptr, q["moved"], q["obs"],
+                                           q["code"], q["done"], q["illegal"], q["ctr"], q["active"], None,
+                                           _lib.stream_handle(self._dev)), "mzh_env_step")
+        return pk
+
+    def _finish_step(self):
+        """the step's results from the staging record (after the synchronisation)"""
+        h = self._pk.h
         self.c_state = tuple(int(x) for x in h["state"][0])
         self.step_counter, self.reset_check = int(h["ctr"][0]), bool(h["active"][0])
         rwd, done_b, illegal_b = _REWARD[int(h["code"][0])], bool(h["done"][0]), bool(h["illegal"][0])

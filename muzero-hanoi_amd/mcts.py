@@ -149,6 +149,11 @@ class MCTS:
         """run_mcts for a network: the draws go straight into the pinned staging buffer (rng.predraw_into),
         and the search arguments -- every device pointer of the staging buffers fixed -- are built once per
         (engine, S, observation width) and only their scalars and optional pointers set per call"""
+        eng, pout = self._launch_fast(state, network, temperature, deterministic, S, bad_t)
+        pout.to_host()
+        return self._finish_fast(pout, temperature, bad_t)
+
+    def _launch_fast(self, state, network, temperature, deterministic, S, bad_t):
         eng = engine_for(network, S, 1)
         x = np.asarray(state).reshape(-1)
         pin, pout, a, addrs = self._prepared(eng, S, x.size)
@@ -177,7 +182,9 @@ class MCTS:
         pt = eng.pow_table(S, float(temperature_k))
         a.pow_table = None if pt is None else pt.data_ptr()
         _lib.check(_lib.lib().mzh_search(eng._h, ctypes.byref(a), _lib.stream_handle(eng.device)), "mzh_search")
-        pout.to_host()
+        return eng, pout
+
+    def _finish_fast(self, pout, temperature, bad_t):
         host = pout.h
         self.min_max_stats.maximum = float(host["minmax"][0, 0])
         self.min_max_stats.minimum = float(host["minmax"][0, 1])
@@ -190,6 +197,29 @@ class MCTS:
         if bad_t:
             raise ValueError(f"Expect `temperature` to be in the range [0.0, 1.0], got {temperature}")
         return int(host["action"][0]), host["pi"][0].astype(np.float64), float(host["root_q"][0])
+
+    def run_mcts_step(self, state, network, temperature, deterministic, env):
+        """run_mcts(state, ...) followed by env.step(action) (Muzero._play_game's pair of calls,
+        Muzero.py:165-175) as two chained launches and ONE synchronisation: the env kernel reads the
+        action the search kernel wrote.  The same draws, results and env state as the two calls.
+        Returns (action, pi, root_Q, env.step's tuple), or None where run_mcts itself must run (a replayed
+        network, a temperature it refuses, an env not reset, other UCB constants) -- the caller then makes
+        the two calls; with staging through copies or the env on another device the two run one after
+        the other here."""
+        S = int(self.n_simulations)
+        if (isinstance(network, RecordedNetwork) or not 0.0 <= temperature <= 1.0 or not env.reset_check
+                or self.pb_c_base != 19652 or self.pb_c_init != 1.25):
+            return None
+        eng, pout = self._launch_fast(state, network, temperature, deterministic, S, False)
+        pk = env._packed()
+        if pout.zero_copy and pk.zero_copy and torch.device(eng.device) == env._dev:
+            env._launch_step(action_ptr=pout.dptr["action"])
+            _lib.synchronize(eng.device)
+            action, pi, q = self._finish_fast(pout, temperature, False)
+            return action, pi, q, env._finish_step()
+        pout.to_host()  # staging with copies: the two calls one after the other
+        action, pi, q = self._finish_fast(pout, temperature, False)
+        return action, pi, q, env.step(action)
 
     def _prepared(self, eng, S, in_dim):
         """zero-copy staging buffers (the search kernel reads its inputs from and writes its outputs to pinned

@@ -57,9 +57,15 @@ def play_game(env, mcts, network, episode, deterministic=False, *, discount=0.8,
     done = False
     step = 0
     T = adjust_temperature(episode) if temperature is None else temperature
+    # our MCTS + TowersOfHanoi: the search and the env step as chained launches with one synchronisation
+    chain = getattr(mcts, "run_mcts_step", None) if hasattr(env, "_launch_step") else None
     while not done:
-        action, pi_prob, rootQ = mcts.run_mcts(c_state, network, temperature=T, deterministic=deterministic)
-        n_state, rwd, done, _ = env.step(action)
+        r = chain(c_state, network, T, deterministic, env) if chain is not None else None
+        if r is not None:
+            action, pi_prob, rootQ, (n_state, rwd, done, _) = r
+        else:
+            action, pi_prob, rootQ = mcts.run_mcts(c_state, network, temperature=T, deterministic=deterministic)
+            n_state, rwd, done, _ = env.step(action)
         step += 1
         episode_state.append(c_state)
         episode_action.append(action)
