@@ -116,6 +116,18 @@ class TowersOfHanoi:
             self._ptrs = self._pk.dptr  # fixed: the call passes them as is
         return self._pk
 
+    def _packed_out2(self):
+        """a second record of the step's outputs (MCTS.play_episode alternates output records between decisions)"""
+        if getattr(self, "_pk2", None) is None:
+            n = self.discs
+            fields = [("moved", torch.uint8, (1, n)), ("obs", torch.float32, (1, 3 * n)), ("code", torch.int8, (1,)),
+                      ("done", torch.uint8, (1,)), ("illegal", torch.uint8, (1,))]
+            try:
+                self._pk2 = Packed(fields, self._dev, zero_copy=True)
+            except RuntimeError:
+                self._pk2 = Packed(fields, self._dev)
+        return self._pk2
+
     def _encode(self, state):
         st = torch.tensor([list(state)], dtype=torch.uint8, device=self._dev)
         return engine.encode_obs(self.discs, st)[0].to(torch.float64).cpu().numpy()

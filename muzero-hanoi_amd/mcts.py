@@ -20,6 +20,8 @@ from . import rng as _rng
 from .networks import engine_for
 from .staging import Packed
 
+_ENV_REWARD = {0: 0, 1: 100, -1: -100 / 1000}  # mzh_env_step codes -> the reference's rewards (env.py)
+
 
 _REPLAY_ENGINES = {}
 
@@ -220,6 +222,134 @@ class MCTS:
         pout.to_host()  # staging with copies: the two calls one after the other
         action, pi, q = self._finish_fast(pout, temperature, False)
         return action, pi, q, env.step(action)
+
+    def play_episode(self, env, network, temperature, deterministic):
+        """Muzero._play_game's decision loop (run_mcts then env.step until done, Muzero.py:165-186) with the
+        decisions pipelined on the device: decision k+1's search reads its observation from decision k's env
+        kernel and its MinMaxStats from decision k's search, so it is launched (with its env step) BEFORE the
+        host waits for decision k -- the GPU runs decision after decision while the host records the last one.
+        When decision k ends the episode, the speculative decision k+1 is discarded: its env step meets an
+        inactive env (left untouched, as the kernel's AssertionError path does) and the NumPy stream is put back
+        to where decision k left it.  The same draws, results, MinMaxStats and env state as the per-decision calls
+        (tests/test_selfplay.py).  Returns (steps, obs list, actions, rewards, pis, root Qs) or None where the
+        pipeline does not apply (then the caller makes the per-decision calls)."""
+        S = int(self.n_simulations)
+        rs = np.random.mtrand._rand
+        bg = rs._bit_generator
+        if (isinstance(network, RecordedNetwork) or not 0.0 <= temperature <= 1.0 or not env.reset_check
+                or self.pb_c_base != 19652 or self.pb_c_init != 1.25 or type(bg).__name__ != "MT19937"
+                or (_rng.uses_noise(deterministic, self.root_dirichlet_alpha, self.root_exploration_eps)
+                    and not 0.0 < float(self.root_dirichlet_alpha) <= 1.0)):
+            return None
+        eng = engine_for(network, S, 1)
+        x0 = np.asarray(env.oneH_c_state if hasattr(env, "oneH_c_state") else None)
+        sets = self._prepared2(eng, S, env.discs * 3)
+        ek, eo = env._packed(), env._packed_out2()
+        if not all(p.zero_copy for st in sets for p in st[:2]) or not (ek.zero_copy and eo.zero_copy) \
+                or torch.device(eng.device) != env._dev or x0.shape != (env.discs * 3,):
+            return None
+        stream = _lib.stream_handle(eng.device)
+        L = _lib.lib()
+        pt = eng.pow_table(S, float(temperature))
+        flags = _lib.MZH_FLAG_NP1_UCB if self.np1_ucb else 0
+        outs = [(ek.h, ek.dptr), (eo.h, eo.dptr)]  # env output records, alternating
+        q = ek.dptr  # state / ctr / active: one record, updated in place decision after decision
+        eh = ek.h
+        eh["state"][0] = env.c_state
+        eh["ctr"][0] = env.step_counter
+        eh["active"][0] = 1
+        mt = ctypes.c_char * 2500  # struct mt19937_state {uint32 key[624]; int pos}
+        saved = mt()
+        st_addr = bg.ctypes.state_address
+        evs = [torch.cuda.Event(), torch.cuda.Event()]
+
+        def launch(k):
+            pin, pout, a, addrs = sets[k % 2]
+            h = pin.h
+            noisy, drew_u = _rng.predraw_into(h["noise"], h["tie"], h["u"], deterministic=deterministic,
+                                              alpha=self.root_dirichlet_alpha, eps=self.root_exploration_eps,
+                                              draw_action=True, addrs=addrs)
+            if k == 0:
+                h["obs"][0] = x0
+                h["mm"][0] = (self.min_max_stats.maximum, self.min_max_stats.minimum)
+                a.obs, a.minmax_in = pin.dptr["obs"], pin.dptr["mm"]
+            else:  # the previous decision's env observation and search MinMaxStats, on the device
+                a.obs = outs[(k - 1) % 2][1]["obs"]
+                a.minmax_in = sets[(k - 1) % 2][1].dptr["minmax"]
+            a.n_sims, a.discount, a.eps = S, float(self.discount), float(self.root_exploration_eps)
+            a.temperature, a.deterministic, a.flags = float(temperature), 1 if deterministic else 0, flags
+            a.noise = pin.dptr["noise"] if noisy else None
+            a.action_u = pin.dptr["u"] if drew_u else None
+            a.pow_table = None if pt is None else pt.data_ptr()
+            _lib.check(L.mzh_search(eng._h, ctypes.byref(a), stream), "mzh_search")
+            o = outs[k % 2][1]
+            _lib.check(L.mzh_env_step(env.discs, env.goal_peg, env.max_steps, 1, q["state"], pout.dptr["action"],
+                                      o["moved"], o["obs"], o["code"], o["done"], o["illegal"], q["ctr"], q["active"],
+                                      None, stream), "mzh_env_step")
+            evs[k % 2].record(torch.cuda.current_stream(eng.device))
+
+        obs_l, act_l, rwd_l, pi_l, q_l = [x0.astype(np.float64)], [], [], [], []
+        launch(0)
+        k = 0
+        while True:
+            ctypes.memmove(saved, st_addr, 2500)  # the stream before the speculative next decision's draws
+            launch(k + 1)
+            evs[k % 2].synchronize()
+            pout = sets[k % 2][1]
+            ph, oh = pout.h, outs[k % 2][0]
+            self.min_max_stats.maximum = float(ph["minmax"][0, 0])
+            self.min_max_stats.minimum = float(ph["minmax"][0, 1])
+            n = int(ph["latent_len"][0])
+            self._latent_host = [int(m) for m in ph["latent"][0, :n]]
+            self.last_extra_ties = int(ph["extra_ties"][0])
+            if self.last_extra_ties:
+                warnings.warn("search met an argmax tie beyond the root's first selection: the NumPy RNG stream "
+                              "now differs from the reference's", RuntimeWarning)
+            act_l.append(int(ph["action"][0]))
+            pi_l.append(ph["pi"][0].astype(np.float64))
+            q_l.append(float(ph["root_q"][0]))
+            rwd_l.append(_ENV_REWARD[int(oh["code"][0])])
+            done = bool(oh["done"][0])
+            if done:
+                ctypes.memmove(st_addr, saved, 2500)  # the discarded decision's draws never happened
+                evs[(k + 1) % 2].synchronize()  # it ran on an inactive env: state, counter untouched
+                break
+            obs_l.append(oh["obs"][0].astype(np.float64))
+            k += 1
+        env.c_state = tuple(int(v) for v in eh["state"][0])
+        env.step_counter, env.reset_check = int(eh["ctr"][0]), bool(eh["active"][0])
+        return k + 1, obs_l, act_l, rwd_l, pi_l, q_l
+
+    def _prepared2(self, eng, S, in_dim):
+        """two sets of zero-copy staging buffers and SearchArgs (play_episode's pipeline alternates them)"""
+        key = (id(eng), S, in_dim)
+        if getattr(self, "_args2_key", None) != key:
+            sets = []
+            for _ in range(2):
+                fin = [("obs", torch.float32, (1, in_dim)), ("noise", torch.float64, (1, 6)),
+                       ("tie", torch.int32, (1,)), ("u", torch.float64, (1,)), ("mm", torch.float64, (1, 2))]
+                fout = [("visits", torch.int32, (1, 6)), ("root_q", torch.float64, (1,)),
+                        ("minmax", torch.float64, (1, 2)), ("extra_ties", torch.int32, (1,)),
+                        ("action", torch.int32, (1,)), ("pi", torch.float64, (1, 6)),
+                        ("latent", torch.int32, (1, S + 1)), ("latent_len", torch.int32, (1,)),
+                        ("sel_steps", torch.int32, (1,))]
+                try:
+                    pin, pout = Packed(fin, eng.device, zero_copy=True), Packed(fout, eng.device, zero_copy=True)
+                except RuntimeError:
+                    pin, pout = Packed(fin, eng.device), Packed(fout, eng.device)
+                a = _lib.SearchArgs()
+                a.B = 1
+                a.tie_idx = pin.dptr["tie"]
+                o = pout.dptr
+                for k, f in (("visits", "visits"), ("root_q", "root_q"), ("minmax_out", "minmax"),
+                             ("extra_ties", "extra_ties"), ("action", "action"), ("pi", "pi"), ("latent", "latent"),
+                             ("latent_len", "latent_len"), ("sel_steps", "sel_steps")):
+                    setattr(a, k, o[f])
+                h = pin.h
+                sets.append((pin, pout, a, (h["noise"].ctypes.data, h["tie"].ctypes.data, h["u"].ctypes.data)))
+            self._sets2 = sets
+            self._args2_key = key
+        return self._sets2
 
     def _prepared(self, eng, S, in_dim):
         """zero-copy staging buffers (the search kernel reads its inputs from and writes its outputs to pinned

@@ -57,8 +57,15 @@ def play_game(env, mcts, network, episode, deterministic=False, *, discount=0.8,
     done = False
     step = 0
     T = adjust_temperature(episode) if temperature is None else temperature
-    # our MCTS + TowersOfHanoi: the search and the env step as chained launches with one synchronisation
-    chain = getattr(mcts, "run_mcts_step", None) if hasattr(env, "_launch_step") else None
+    # our MCTS + TowersOfHanoi: the decisions pipelined on the device (MCTS.play_episode), else the search and
+    # the env step as chained launches with one synchronisation per decision (MCTS.run_mcts_step)
+    ours = hasattr(env, "_launch_step")
+    pipe = getattr(mcts, "play_episode", None) if ours else None
+    r = pipe(env, network, T, deterministic) if pipe is not None and c_state is env.oneH_c_state else None
+    if r is not None:
+        step, episode_state, episode_action, episode_rwd, episode_piProb, episode_rootQ = r
+        done = True
+    chain = getattr(mcts, "run_mcts_step", None) if ours else None
     while not done:
         r = chain(c_state, network, T, deterministic, env) if chain is not None else None
         if r is not None:

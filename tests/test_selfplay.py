@@ -174,32 +174,39 @@ def test_batched_b1_equals_play_game():
 
 
 @pytest.mark.gpu
-def test_play_game_chained_equals_separate_calls(monkeypatch):
-    """play_game chains each run_mcts with its env.step (MCTS.run_mcts_step: the env kernel reads the search
-    kernel's action, one synchronisation): the same episode, MinMaxStats, env state and NumPy stream as
-    the two separate calls."""
+@pytest.mark.parametrize("deterministic", [False, True])
+def test_play_game_pipelined_and_chained_equal_separate_calls(monkeypatch, deterministic):
+    """play_game pipelines the decisions on the device (MCTS.play_episode: decision k+1 launched from decision k's
+    device outputs before the host waits for k; the speculative decision after the last one discarded, the
+    NumPy stream put back) or chains each run_mcts with its env.step (MCTS.run_mcts_step): the same episodes,
+    MinMaxStats, latent actions, env state and NumPy stream as the separate calls -- over several episodes,
+    including max_steps endings."""
     from muzero_hanoi_amd.env import TowersOfHanoi
     from muzero_hanoi_amd.mcts import MCTS
     from muzero_hanoi_amd.selfplay import play_game
 
-    n, S, max_steps = 3, 25, 60
+    n, S, max_steps = 3, 25, 30
     net = _fresh_net(n, seed=3)
     outs = []
-    for chained in (True, False):
-        if not chained:
+    for mode in ("pipelined", "chained", "separate"):
+        if mode != "pipelined":
+            monkeypatch.setattr(MCTS, "play_episode", lambda *a, **k: None)
+        if mode == "separate":
             monkeypatch.setattr(MCTS, "run_mcts_step", lambda *a, **k: None)
         env = TowersOfHanoi(N=n, max_steps=max_steps, init_state_idx=2)
         mcts = MCTS(discount=0.8, root_dirichlet_alpha=0.25, n_simulations=S, batch_s=256, device="cpu")
         np.random.seed(77)
-        res = [play_game(env, mcts, net, episode=e, deterministic=False, n_step=10) for e in (100, 900)]
+        res = [play_game(env, mcts, net, episode=e, deterministic=deterministic, n_step=10)
+               for e in (100, 900, 1500, 2500)]
         outs.append((res, np.random.random_sample(3), mcts.min_max_stats.maximum, mcts.min_max_stats.minimum,
-                     env.c_state, env.step_counter, env.reset_check))
-    (ra, rnga, *sa), (rb, rngb, *sb) = outs
-    for ea, eb in zip(ra, rb):
-        assert ea[0] == eb[0]
-        for x, y in zip(ea[1:], eb[1:]):
-            assert np.array_equal(np.asarray(x), np.asarray(y))
-    assert np.array_equal(rnga, rngb) and sa == sb
+                     [int(t) for t in mcts.return_latent_actions()], env.c_state, env.step_counter, env.reset_check))
+    ref = outs[-1]
+    for got in outs[:-1]:
+        for ea, eb in zip(got[0], ref[0]):
+            assert ea[0] == eb[0]
+            for x, y in zip(ea[1:], eb[1:]):
+                assert np.array_equal(np.asarray(x), np.asarray(y))
+        assert np.array_equal(got[1], ref[1]) and got[2:] == ref[2:]
 
 
 @pytest.mark.gpu
