@@ -103,8 +103,11 @@ def _host(x):
 @pytest.mark.gpu
 @pytest.mark.parametrize("size,fill,kind,m", [(1, 1, "uniform", 4), (300, 200, "uniform", 64), (5000, 7000, "heavy", 256),
                                               (50000, 50000, "uniform", 256), (50000, 50000, "tiny", 256),
-                                              (70001, 70001, "zeros", 4096), (20000, 12345, "heavy", 1)])
+                                              (70001, 70001, "zeros", 4096), (20000, 12345, "heavy", 1),
+                                              (300000, 300000, "uniform", 256)])
 def test_device_draw_equals_host_draw(size, fill, kind, m):
+    """300,000 transitions: two block passes of np.sum's order and binary steps in HBM before the search
+    window (the cdf sample's stride above 16)"""
     host, dev = _pair(size, fill, size + m, kind)
     assert np.array_equal(dev.priorities, host.priorities)
     for step in range(3):
